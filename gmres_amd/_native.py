@@ -1,0 +1,122 @@
+"""ctypes bindings of the in-tree native libraries.
+
+libgmres_hip.so   -- HIP kernels + C-ABI (include/gmres_hip.h)
+libgmres_fhost.so -- Fortran host drivers (gmres_amd/fortran/gmres_hip.f90)
+
+There is no fallback: if a library is missing the import of the solver API
+raises, so a GPU run can never silently execute anything but the HIP path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG, "lib")
+HIP_SO = os.path.join(LIB_DIR, "libgmres_hip.so")
+FHOST_SO = os.path.join(LIB_DIR, "libgmres_fhost.so")
+HEADER = os.path.join(os.path.dirname(PKG), "include", "gmres_hip.h")
+
+GK_OK = 0
+GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
+GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER = range(6)
+KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other"]
+
+c_int, c_double, c_ll, c_vp = ctypes.c_int, ctypes.c_double, ctypes.c_longlong, ctypes.c_void_p
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+_hip = None
+_fhost = None
+
+
+class GkError(RuntimeError):
+    pass
+
+
+def header_symbols() -> list[str]:
+    """Every function the C-ABI header declares."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(gk_\w+)\s*\(", txt, re.M)))
+
+
+_SIGS = {
+    "gk_last_error": (ctypes.c_char_p, []),
+    "gk_version": (c_int, []),
+    "gk_create": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_vp)]),
+    "gk_destroy": (c_int, [c_vp]),
+    "gk_comm_unique_id": (c_int, [ctypes.c_char_p]),
+    "gk_comm_init": (c_int, [c_vp, c_int, c_int, c_int, ctypes.c_char_p]),
+    "gk_local_size": (c_int, [c_vp, ctypes.POINTER(c_ll)]),
+    "gk_set_precond": (c_int, [c_vp, c_int, _dp, c_int, c_int]),
+    "gk_set_rhs": (c_int, [c_vp, _dp]),
+    "gk_set_rhs_ones": (c_int, [c_vp]),
+    "gk_rhs_norm": (c_int, [c_vp, _dp]),
+    "gk_zero_x": (c_int, [c_vp]),
+    "gk_get_x": (c_int, [c_vp, _dp]),
+    "gk_set_x": (c_int, [c_vp, _dp]),
+    "gk_apply": (c_int, [c_vp, c_int, _dp, _dp]),
+    "gk_true_residual": (c_int, [c_vp, _dp]),
+    "gk_mgs_cycle_start": (c_int, [c_vp, _dp]),
+    "gk_mgs_step": (c_int, [c_vp, c_int, _dp]),
+    "gk_update_x": (c_int, [c_vp, _dp, c_int]),
+    "gk_mgs_verr": (c_int, [c_vp, c_int, c_int, _dp]),
+    "gk_hh_cycle_start": (c_int, [c_vp, c_int, _dp]),
+    "gk_hh_step": (c_int, [c_vp, c_int, c_int, _dp]),
+    "gk_hh_update_x": (c_int, [c_vp, _dp, c_int]),
+    "gk_hh_verr": (c_int, [c_vp, c_int, _dp]),
+    "gk_profile_enable": (c_int, [c_vp, c_int]),
+    "gk_profile_reset": (c_int, [c_vp]),
+    "gk_profile_read": (c_int, [c_vp, c_int, _dp, ctypes.POINTER(c_ll)]),
+    "gk_sync": (c_int, [c_vp]),
+    "gk_poisson5": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "gk_precond_apply": (c_int, [c_int, c_int, _dp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "gk_mgs_project": (c_int, [c_ll, c_vp, c_vp, c_vp, c_vp]),
+    "gk_dot": (c_int, [c_ll, c_vp, c_vp, c_vp, c_vp]),
+}
+
+_FSIGS = {
+    "gmres_mgsr_hip_run": (c_int, [c_vp, c_int, c_double, c_int, c_int, _dp, _dp, _dp, _ip, _ip, c_int, c_int,
+                                   _dp, _dp, _ip]),
+    "gmres_hh_hip_run": (c_int, [c_vp, c_int, c_double, c_int, c_int, c_int, _dp, _dp, _dp, _ip, _ip, c_int,
+                                 c_int, _dp, _dp, _ip]),
+}
+
+
+def _load(path: str, what: str) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise GkError(f"{what} not built at {path}: run `python -m gmres_amd.build` "
+                      "(or __graft_entry__.build()); there is no CPU fallback")
+    return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def hip() -> ctypes.CDLL:
+    global _hip
+    if _hip is None:
+        L = _load(HIP_SO, "libgmres_hip.so")
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _hip = L
+    return _hip
+
+
+def fhost() -> ctypes.CDLL:
+    global _fhost
+    if _fhost is None:
+        hip()
+        L = _load(FHOST_SO, "libgmres_fhost.so")
+        for name, (res, args) in _FSIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _fhost = L
+    return _fhost
+
+
+def check(status: int, what: str) -> None:
+    if status != GK_OK:
+        msg = hip().gk_last_error()
+        raise GkError(f"{what} failed (status {status}): {msg.decode() if msg else ''}")

@@ -1,0 +1,1076 @@
+// gk_api.hip -- C-ABI implementation of include/gmres_hip.h (libgmres_hip.so).
+//
+// One context per GPU (one process per GPU on a node).  A context owns the
+// slab of grid lines [line0, line0+nlines) of every vector, the Krylov basis
+// V (n_loc x (m+1), column stride padded to 256 B) and the reduction slabs,
+// all resident in HBM for the whole solve; the host sees only the (j+1)
+// Hessenberg entries of each Arnoldi step.  All work is issued on one HIP
+// stream per context; on N GPUs the dot-product slabs are RCCL all-reduced
+// and the stencil halos exchanged point-to-point on that same stream.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gmres_hip.h"
+#include "gk_kernels.hpp"
+
+using gk::i64;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(call)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (call);                                                                 \
+        if (e_ != hipSuccess) return set_err(GK_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #call, \
+                                             hipGetErrorString(e_));                            \
+    } while (0)
+#define NCCLCHK(call)                                                                           \
+    do {                                                                                        \
+        ncclResult_t r_ = (call);                                                               \
+        if (r_ != ncclSuccess) return set_err(GK_ERR_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #call, \
+                                              ncclGetErrorString(r_));                          \
+    } while (0)
+#define CHK(call)                      \
+    do {                               \
+        int s_ = (call);               \
+        if (s_ != GK_OK) return s_;    \
+    } while (0)
+#define LAUNCHCHK() HIPCHK(hipGetLastError())
+
+constexpr int NSLOT = 4;  // partial slabs (ping-pong + spares)
+constexpr int PROF_POOL = 8192;
+
+i64 round_up(i64 a, i64 b) { return (a + b - 1) / b * b; }
+
+}  // namespace
+
+struct gk_ctx {
+    int dev = 0, N = 0, line0 = 0, nlines = 0, m = 0;
+    i64 nloc = 0, ld = 0, g0 = 0;
+    hipStream_t st = nullptr;
+    // HBM residents
+    double *V = nullptr;  // (m+1) columns, stride ld
+    double *w = nullptr, *z = nullptr, *aux = nullptr, *dA = nullptr, *dB = nullptr;
+    double *x = nullptr, *b = nullptr, *vj = nullptr, *hlo = nullptr, *hhi = nullptr;
+    double *red = nullptr;   // NSLOT * NPMAX partial slabs
+    double *hcol = nullptr;  // m+2 Hessenberg column / scalars
+    double *ydev = nullptr;  // m+1
+    double *hb = nullptr;    // m+2 Householder broadcast buffer
+    double *scal = nullptr;  // 8 scalars
+    double *hcol_host = nullptr;  // pinned
+    double *Vb = nullptr;    // Householder verr basis (lazy)
+    double *gram_slab = nullptr, *gram_out = nullptr;
+    short2 *gram_pairs = nullptr;
+    int gram_nblk = 0;
+    // preconditioner
+    int pkind = GK_PREC_IDENTITY, pdeg = 8;
+    double p0 = 8.2, p1 = 0.2;
+    // decomposition / comm
+    int nranks = 1, rank = 0, max_lines = 0;
+    ncclComm_t comm = nullptr;
+    bool comm_ok = false;
+    // launch geometry
+    int vec = 2, JT = 16;
+    dim3 sgrid;
+    int np_st = 0, np_pj = 0, nblk_stream = 0;
+    // state
+    bool cycle_mgs = false, cycle_hh = false;
+    double beta0 = -1.0;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev0, ev1;
+    std::vector<int> evk;
+    int nev = 0;
+    double prof_ms[GK_NKID] = {0};
+    long long prof_n[GK_NKID] = {0};
+};
+
+namespace {
+
+// ------------------------------------------------------------- profiling ---
+int prof_harvest(gk_ctx *c) {
+    if (c->nev == 0) return GK_OK;
+    HIPCHK(hipEventSynchronize(c->ev1[c->nev - 1]));
+    for (int k = 0; k < c->nev; ++k) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, c->ev0[k], c->ev1[k]));
+        c->prof_ms[c->evk[k]] += ms;
+        c->prof_n[c->evk[k]] += 1;
+    }
+    c->nev = 0;
+    return GK_OK;
+}
+
+struct ProfScope {
+    gk_ctx *c;
+    int slot = -1;
+    ProfScope(gk_ctx *c_, int kid) : c(c_) {
+        if (!c->prof) return;
+        if (c->nev == PROF_POOL) prof_harvest(c);
+        slot = c->nev++;
+        c->evk[slot] = kid;
+        (void)hipEventRecord(c->ev0[slot], c->st);
+    }
+    ~ProfScope() {
+        if (slot >= 0) (void)hipEventRecord(c->ev1[slot], c->st);
+    }
+};
+
+double *slot(gk_ctx *c, int s) { return c->red + (i64)s * gk::NPMAX; }
+
+// ----------------------------------------------------------------- comm ---
+int allreduce(gk_ctx *c, double *buf, int count) {
+    if (c->nranks == 1) return GK_OK;
+    ProfScope ps(c, GK_KID_COMM);
+    NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->st));
+    return GK_OK;
+}
+
+int bcast(gk_ctx *c, double *buf, int count, int root) {
+    if (c->nranks == 1) return GK_OK;
+    ProfScope ps(c, GK_KID_COMM);
+    NCCLCHK(ncclBroadcast(buf, buf, count, ncclDouble, root, c->comm, c->st));
+    return GK_OK;
+}
+
+// Exchange the first / last local grid line of vec with the slab neighbours.
+int halo(gk_ctx *c, const double *vec) {
+    if (c->nranks == 1) return GK_OK;
+    ProfScope ps(c, GK_KID_COMM);
+    const int N = c->N;
+    NCCLCHK(ncclGroupStart());
+    if (c->rank > 0) {
+        NCCLCHK(ncclSend(vec, N, ncclDouble, c->rank - 1, c->comm, c->st));
+        NCCLCHK(ncclRecv(c->hlo, N, ncclDouble, c->rank - 1, c->comm, c->st));
+    }
+    if (c->rank < c->nranks - 1) {
+        NCCLCHK(ncclSend(vec + (i64)(c->nlines - 1) * N, N, ncclDouble, c->rank + 1, c->comm, c->st));
+        NCCLCHK(ncclRecv(c->hhi, N, ncclDouble, c->rank + 1, c->comm, c->st));
+    }
+    NCCLCHK(ncclGroupEnd());
+    return GK_OK;
+}
+
+const double *halo_lo(gk_ctx *c) { return (c->nranks > 1 && c->rank > 0) ? c->hlo : nullptr; }
+const double *halo_hi(gk_ctx *c) { return (c->nranks > 1 && c->rank < c->nranks - 1) ? c->hhi : nullptr; }
+
+// -------------------------------------------------------------- geometry ---
+void set_geometry(gk_ctx *c) {
+    const int N = c->N;
+    c->vec = (N % 2 == 0) ? 2 : 1;
+    const int gx = (N + gk::TPB * c->vec - 1) / (gk::TPB * c->vec);
+    const int ml = c->max_lines > 0 ? c->max_lines : c->nlines;
+    // ~2048 workgroups for the stencil sweeps, marching JT lines each
+    int JT = (int)std::max<i64>(1, ((i64)ml * gx + 2047) / 2048);
+    if (JT > 64) JT = 64;
+    int gy = (ml + JT - 1) / JT;
+    while ((i64)gx * gy > gk::NPMAX) {
+        ++JT;
+        gy = (ml + JT - 1) / JT;
+    }
+    c->JT = JT;
+    c->sgrid = dim3(gx, gy, 1);
+    c->np_st = gx * gy;
+    // projection kernels: fixed workgroup count derived from the largest slab
+    const i64 nmax2 = ((i64)ml * N + 1) / 2;
+    i64 npj = (nmax2 + (i64)gk::TPB * gk::UNR - 1) / ((i64)gk::TPB * gk::UNR);
+    if (npj > 2048) npj = 2048;
+    if (npj < 1) npj = 1;
+    c->np_pj = (int)npj;
+    // elementwise kernels: also from the largest slab (their partial slabs are all-reduced)
+    i64 nb = (nmax2 + gk::TPB - 1) / gk::TPB;
+    c->nblk_stream = (int)std::min<i64>(std::max<i64>(nb, 1), 2048);
+}
+
+// -------------------------------------------------------------- launches ---
+template <int VEC, int OP, int ACC>
+int launch_stencil_v(gk_ctx *c, const gk::StArgs &a) {
+    gk::k_stencil<VEC, OP, ACC><<<c->sgrid, gk::TPB, 0, c->st>>>(a);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
+template <int OP, int ACC>
+int launch_stencil_o(gk_ctx *c, const gk::StArgs &a) {
+    return c->vec == 2 ? launch_stencil_v<2, OP, ACC>(c, a) : launch_stencil_v<1, OP, ACC>(c, a);
+}
+
+template <int OP>
+int launch_stencil_a(gk_ctx *c, int acc, const gk::StArgs &a) {
+    if (acc == gk::ACC_NONE) return launch_stencil_o<OP, gk::ACC_NONE>(c, a);
+    if (acc == gk::ACC_DOT) return launch_stencil_o<OP, gk::ACC_DOT>(c, a);
+    return launch_stencil_o<OP, gk::ACC_NORM>(c, a);
+}
+
+int stencil(gk_ctx *c, int op, int acc, gk::StArgs a) {
+    ProfScope ps(c, GK_KID_STENCIL);
+    a.hlo = halo_lo(c);
+    a.hhi = halo_hi(c);
+    a.N = c->N;
+    a.nlines = c->nlines;
+    a.JT = c->JT;
+    switch (op) {
+        case gk::OP_PLAIN: return launch_stencil_a<gk::OP_PLAIN>(c, acc, a);
+        case gk::OP_RESID: return launch_stencil_a<gk::OP_RESID>(c, acc, a);
+        case gk::OP_CBPR2: return launch_stencil_a<gk::OP_CBPR2>(c, acc, a);
+        case gk::OP_CHEB_FIRST: return launch_stencil_a<gk::OP_CHEB_FIRST>(c, acc, a);
+        default: return launch_stencil_a<gk::OP_CHEB_ITER>(c, acc, a);
+    }
+}
+
+int proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
+         int npin, double *pout, double *hslot, double coef, i64 tail0 = 0) {
+    ProfScope ps(c, GK_KID_PROJ);
+    const dim3 g(c->np_pj);
+    const i64 n = c->nloc;
+    switch (mode) {
+        case gk::PJ_DOT:
+            gk::k_proj<gk::PJ_DOT><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
+            break;
+        case gk::PJ_AXPY:
+            gk::k_proj<gk::PJ_AXPY><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
+            break;
+        case gk::PJ_AXPY_DOT:
+            gk::k_proj<gk::PJ_AXPY_DOT><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
+            break;
+        default:
+            gk::k_proj<gk::PJ_AXPY_NORM><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
+            break;
+    }
+    LAUNCHCHK();
+    return GK_OK;
+}
+
+int scale(gk_ctx *c, double *out, const double *w, const double *pin, int npin, double *hslot) {
+    ProfScope ps(c, GK_KID_SCALE);
+    gk::k_scale<<<c->nblk_stream, gk::TPB, 0, c->st>>>(out, w, pin, npin, hslot, c->nloc);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
+int finalize(gk_ctx *c, const double *pin, int npin, double *out, int take_sqrt) {
+    ProfScope ps(c, GK_KID_OTHER);
+    gk::k_finalize<<<1, gk::TPB, 0, c->st>>>(pin, npin, out, take_sqrt);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
+int d2h_sync(gk_ctx *c, double *host, const double *dev, int count) {
+    HIPCHK(hipMemcpyAsync(c->hcol_host, dev, sizeof(double) * count, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (c->prof) CHK(prof_harvest(c));
+    std::memcpy(host, c->hcol_host, sizeof(double) * count);
+    return GK_OK;
+}
+
+int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *part);
+
+// out = M^-1 (A v)  or  out = M^-1 (b - A v) (resid); the LAST sweep carries
+// the fused reduction `acc` (dot with vdot, or norm) into slab `part`.
+// Reference: gmres_mgsr.f90:336-337 (step), :314-320 (cycle start).
+int op_precond(gk_ctx *c, const double *v, double *out, bool resid, int acc, const double *vdot,
+               double *part) {
+    CHK(halo(c, v));
+    gk::StArgs a{};
+    if (c->pkind == GK_PREC_IDENTITY) {
+        a.x = v;
+        a.in1 = c->b;
+        a.y = out;
+        a.vdot = vdot;
+        a.part = part;
+        return stencil(c, resid ? gk::OP_RESID : gk::OP_PLAIN, acc, a);
+    }
+    // z = A v   (or b - A v)
+    a.x = v;
+    a.in1 = c->b;
+    a.y = c->z;
+    CHK(stencil(c, resid ? gk::OP_RESID : gk::OP_PLAIN, gk::ACC_NONE, a));
+    return precond_sweeps(c, out, acc, vdot, part);
+}
+
+// out = M^-1 z for z already in c->z (cbpr2 or Chebyshev sweeps).
+int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *part) {
+    CHK(halo(c, c->z));
+    if (c->pkind == GK_PREC_CBPR2) {
+        // cbpr2 coefficients exactly as chebyshev.f90:19-25
+        const double em = c->p0, eM = c->p1;
+        const double cc = (eM - em) / 2.0;
+        const double d = (eM + em) / 2.0;
+        double alpha = 1.0 / d;
+        double beta = cc * alpha / 2.0;
+        beta = beta * beta;
+        alpha = 1.0 / (d - beta);
+        gk::StArgs b2{};
+        b2.x = c->z;
+        b2.y = out;
+        b2.vdot = vdot;
+        b2.part = part;
+        b2.s1 = d;
+        b2.s2 = alpha;
+        return stencil(c, gk::OP_CBPR2, acc, b2);
+    }
+    // Chebyshev(k): k sweeps, each one stencil on d_k fused with the three
+    // vector updates (res, d, z); the first sweep builds d_0 = r/theta on load.
+    const double theta = (c->p0 + c->p1) / 2.0;
+    const double delta = std::fabs(c->p1 - c->p0) / 2.0;
+    const double sigma = theta / delta;
+    double rho0 = delta / theta;
+    double *dcur = c->dA, *dnext = c->dB;
+    for (int it = 0; it < c->pdeg; ++it) {
+        const double rho1 = 1.0 / (2.0 * sigma - rho0);
+        const double c1 = rho1 * rho0, c2 = 2.0 * rho1 / delta;
+        const bool last = (it == c->pdeg - 1);
+        gk::StArgs s{};
+        s.y = out;
+        s.s2 = c1;
+        s.s3 = c2;
+        s.vdot = vdot;
+        s.part = part;
+        if (it == 0) {
+            s.x = c->z;
+            s.s1 = theta;
+            s.o_res = last ? nullptr : c->aux;
+            s.o_d = last ? nullptr : dcur;
+            CHK(stencil(c, gk::OP_CHEB_FIRST, last ? acc : gk::ACC_NONE, s));
+        } else {
+            CHK(halo(c, dcur));
+            s.x = dcur;
+            s.in1 = c->aux;
+            s.in2 = out;
+            s.o_res = last ? nullptr : c->aux;
+            s.o_d = last ? nullptr : dnext;
+            CHK(stencil(c, gk::OP_CHEB_ITER, last ? acc : gk::ACC_NONE, s));
+            std::swap(dcur, dnext);
+        }
+        rho0 = rho1;
+    }
+    return GK_OK;
+}
+
+int owner_of(gk_ctx *c, i64 gidx) {
+    // ranks own consecutive slabs; rank r owns [g0_r, g0_r + nloc_r). Only the
+    // HH path needs this and only for gidx <= m, which lives on the rank whose
+    // slab starts at line 0 when N >= m+1 (checked at cycle start).
+    (void)gidx;
+    return 0;
+}
+
+int check_ctx(gk_ctx *c) {
+    if (c == nullptr) return set_err(GK_ERR_ARG, "null context");
+    if (c->nranks > 1 && !c->comm_ok) return set_err(GK_ERR_STATE, "communicator not initialised");
+    return GK_OK;
+}
+
+int ensure_gram(gk_ctx *c, int ncols) {
+    if (ncols > gk::GCMAX) return set_err(GK_ERR_ARG, "v_err needs <= %d columns", gk::GCMAX);
+    if (c->gram_slab == nullptr) {
+        c->gram_nblk = 512;
+        const int maxpairs = gk::GCMAX * (gk::GCMAX + 1) / 2;
+        HIPCHK(hipMalloc(&c->gram_slab, sizeof(double) * (size_t)c->gram_nblk * maxpairs));
+        HIPCHK(hipMalloc(&c->gram_out, sizeof(double) * maxpairs));
+        HIPCHK(hipMalloc(&c->gram_pairs, sizeof(short2) * maxpairs));
+    }
+    return GK_OK;
+}
+
+// G (host, c x c symmetric, column-major) of the first c columns of base.
+int gram(gk_ctx *c, const double *base, int ncols, std::vector<double> &G) {
+    CHK(ensure_gram(c, ncols));
+    std::vector<short2> pr;
+    for (int bb = 0; bb < ncols; ++bb)
+        for (int aa = 0; aa <= bb; ++aa) pr.push_back(make_short2((short)aa, (short)bb));
+    const int np = (int)pr.size();
+    HIPCHK(hipMemcpyAsync(c->gram_pairs, pr.data(), sizeof(short2) * np, hipMemcpyHostToDevice, c->st));
+    {
+        ProfScope ps(c, GK_KID_OTHER);
+        gk::k_gram<<<c->gram_nblk, gk::TPB, 0, c->st>>>(base, c->ld, ncols, c->nloc, c->gram_pairs, np,
+                                                        c->gram_slab);
+        LAUNCHCHK();
+        gk::k_gram_reduce<<<(np + gk::TPB - 1) / gk::TPB, gk::TPB, 0, c->st>>>(c->gram_slab, c->gram_nblk,
+                                                                            np, c->gram_out);
+        LAUNCHCHK();
+    }
+    CHK(allreduce(c, c->gram_out, np));
+    std::vector<double> flat(np);
+    HIPCHK(hipMemcpyAsync(flat.data(), c->gram_out, sizeof(double) * np, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (c->prof) CHK(prof_harvest(c));
+    G.assign((size_t)ncols * ncols, 0.0);
+    for (int p = 0; p < np; ++p) {
+        G[(size_t)pr[p].y * ncols + pr[p].x] = flat[p];
+        G[(size_t)pr[p].x * ncols + pr[p].y] = flat[p];
+    }
+    return GK_OK;
+}
+
+// v <- P_1 .. P_k v  (apply reflections k..1; hh_step :269-283, update :361-373,
+// calculate_verr :581-585).  The chain's first launch is a pure dot.
+int reflect_chain_down(gk_ctx *c, double *v, int k) {
+    double *P = c->V;
+    int s0 = 0, s1 = 1;
+    CHK(proj(c, gk::PJ_DOT, v, nullptr, P + (i64)(k - 1) * c->ld, nullptr, 0, slot(c, s0), nullptr, 2.0));
+    int np = c->np_pj;
+    for (int i = k; i >= 1; --i) {
+        CHK(allreduce(c, slot(c, s0), np));
+        const double *va = P + (i64)(i - 1) * c->ld;
+        if (i > 1) {
+            CHK(proj(c, gk::PJ_AXPY_DOT, v, va, P + (i64)(i - 2) * c->ld, slot(c, s0), np, slot(c, s1),
+                     nullptr, 2.0));
+            std::swap(s0, s1);
+        } else {
+            CHK(proj(c, gk::PJ_AXPY, v, va, nullptr, slot(c, s0), np, nullptr, nullptr, 2.0));
+        }
+    }
+    return GK_OK;
+}
+
+}  // namespace
+
+// ======================================================================= API
+
+extern "C" {
+
+const char *gk_last_error(void) { return g_err.c_str(); }
+int gk_version(void) { return 1; }
+
+int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out) {
+    if (out == nullptr) return set_err(GK_ERR_ARG, "null out");
+    *out = nullptr;
+    if (nside < 2 || nlines < 1 || line0 < 0 || line0 + nlines > nside || m < 1 || m > 4096)
+        return set_err(GK_ERR_ARG, "bad shape N=%d line0=%d nlines=%d m=%d", nside, line0, nlines, m);
+    HIPCHK(hipSetDevice(device));
+    gk_ctx *c = new gk_ctx();
+    c->dev = device;
+    c->N = nside;
+    c->line0 = line0;
+    c->nlines = nlines;
+    c->m = m;
+    c->nloc = (i64)nside * nlines;
+    c->g0 = (i64)nside * line0;
+    c->ld = round_up(c->nloc, 32);  // 256-byte aligned columns
+    c->max_lines = nlines;
+    set_geometry(c);
+    auto fail = [&](int code) {
+        gk_destroy(c);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess)
+        return fail(set_err(GK_ERR_HIP, "stream create failed"));
+    const size_t vb = sizeof(double) * (size_t)c->ld;
+    if (hipMalloc(&c->V, vb * (m + 1)) != hipSuccess)
+        return fail(set_err(GK_ERR_NOMEM, "cannot allocate V: %.2f GB", vb * (m + 1) / 1e9));
+    double **vecs[] = {&c->w, &c->z, &c->aux, &c->dA, &c->dB, &c->x, &c->b, &c->vj};
+    for (double **p : vecs)
+        if (hipMalloc(p, vb) != hipSuccess) return fail(set_err(GK_ERR_NOMEM, "cannot allocate work vectors"));
+    if (hipMalloc(&c->hlo, sizeof(double) * nside) != hipSuccess ||
+        hipMalloc(&c->hhi, sizeof(double) * nside) != hipSuccess ||
+        hipMalloc(&c->red, sizeof(double) * NSLOT * gk::NPMAX) != hipSuccess ||
+        hipMalloc(&c->hcol, sizeof(double) * (m + 2)) != hipSuccess ||
+        hipMalloc(&c->ydev, sizeof(double) * (m + 1)) != hipSuccess ||
+        hipMalloc(&c->hb, sizeof(double) * (m + 2)) != hipSuccess ||
+        hipMalloc(&c->scal, sizeof(double) * 8) != hipSuccess)
+        return fail(set_err(GK_ERR_NOMEM, "cannot allocate small buffers"));
+    if (hipHostMalloc(&c->hcol_host, sizeof(double) * (m + 2 + gk::GCMAX)) != hipSuccess)
+        return fail(set_err(GK_ERR_NOMEM, "cannot allocate pinned buffer"));
+    if (hipMemsetAsync(c->x, 0, vb, c->st) != hipSuccess || hipMemsetAsync(c->b, 0, vb, c->st) != hipSuccess ||
+        hipMemsetAsync(c->V, 0, vb * (m + 1), c->st) != hipSuccess ||
+        hipMemsetAsync(c->red, 0, sizeof(double) * NSLOT * gk::NPMAX, c->st) != hipSuccess)
+        return fail(set_err(GK_ERR_HIP, "memset failed"));
+    c->ev0.resize(PROF_POOL);
+    c->ev1.resize(PROF_POOL);
+    c->evk.resize(PROF_POOL);
+    for (int k = 0; k < PROF_POOL; ++k) {
+        if (hipEventCreate(&c->ev0[k]) != hipSuccess || hipEventCreate(&c->ev1[k]) != hipSuccess)
+            return fail(set_err(GK_ERR_HIP, "event create failed"));
+    }
+    if (hipStreamSynchronize(c->st) != hipSuccess) return fail(set_err(GK_ERR_HIP, "sync failed"));
+    *out = c;
+    return GK_OK;
+}
+
+int gk_destroy(gk_ctx *c) {
+    if (c == nullptr) return GK_OK;
+    (void)hipSetDevice(c->dev);
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    if (c->comm) ncclCommDestroy(c->comm);
+    double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi,
+                      c->red, c->hcol, c->ydev, c->hb, c->scal, c->Vb, c->gram_slab, c->gram_out};
+    for (double *p : bufs)
+        if (p) (void)hipFree(p);
+    if (c->gram_pairs) (void)hipFree(c->gram_pairs);
+    if (c->hcol_host) (void)hipHostFree(c->hcol_host);
+    for (size_t k = 0; k < c->ev0.size(); ++k) {
+        if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
+        if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
+    }
+    if (c->st) (void)hipStreamDestroy(c->st);
+    delete c;
+    return GK_OK;
+}
+
+int gk_comm_unique_id(unsigned char id[128]) {
+    ncclUniqueId u;
+    NCCLCHK(ncclGetUniqueId(&u));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    std::memcpy(id, &u, 128);
+    return GK_OK;
+}
+
+int gk_comm_init(gk_ctx *c, int nranks, int rank, int max_lines, const unsigned char id[128]) {
+    if (c == nullptr || nranks < 1 || rank < 0 || rank >= nranks || max_lines < c->nlines)
+        return set_err(GK_ERR_ARG, "bad comm args");
+    HIPCHK(hipSetDevice(c->dev));
+    c->nranks = nranks;
+    c->rank = rank;
+    c->max_lines = max_lines;
+    set_geometry(c);
+    if (nranks > 1) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, 128);
+        NCCLCHK(ncclCommInitRank(&c->comm, nranks, u, rank));
+        c->comm_ok = true;
+    }
+    return GK_OK;
+}
+
+int gk_local_size(gk_ctx *c, long long *nloc) {
+    CHK(check_ctx(c));
+    *nloc = c->nloc;
+    return GK_OK;
+}
+
+int gk_set_precond(gk_ctx *c, int kind, const double *params, int nparams, int degree) {
+    CHK(check_ctx(c));
+    if (kind < GK_PREC_IDENTITY || kind > GK_PREC_CHEB) return set_err(GK_ERR_ARG, "bad precond kind %d", kind);
+    if (kind != GK_PREC_IDENTITY && (params == nullptr || nparams < 2))
+        return set_err(GK_ERR_ARG, "precond needs params(1:2)");
+    if (kind == GK_PREC_CHEB && (degree < 1 || degree > 64)) return set_err(GK_ERR_ARG, "bad degree %d", degree);
+    c->pkind = kind;
+    if (params != nullptr && nparams >= 2) {
+        c->p0 = params[0];
+        c->p1 = params[1];
+    }
+    c->pdeg = degree;
+    if (kind == GK_PREC_CHEB && std::fabs(c->p1 - c->p0) == 0.0)
+        return set_err(GK_ERR_ARG, "Chebyshev interval is empty");
+    return GK_OK;
+}
+
+int gk_set_rhs(gk_ctx *c, const double *b) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    HIPCHK(hipMemcpyAsync(c->b, b, sizeof(double) * c->nloc, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->beta0 = -1.0;
+    return GK_OK;
+}
+
+int gk_set_rhs_ones(gk_ctx *c) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    gk::k_fill<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->aux, 1.0, c->nloc);
+    LAUNCHCHK();
+    CHK(halo(c, c->aux));
+    gk::StArgs a{};
+    a.x = c->aux;
+    a.y = c->b;
+    CHK(stencil(c, gk::OP_PLAIN, gk::ACC_NONE, a));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->beta0 = -1.0;
+    return GK_OK;
+}
+
+int gk_rhs_norm(gk_ctx *c, double *beta0) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    CHK(proj(c, gk::PJ_DOT, c->b, nullptr, c->b, nullptr, 0, slot(c, 0), nullptr, 1.0));
+    CHK(allreduce(c, slot(c, 0), c->np_pj));
+    CHK(finalize(c, slot(c, 0), c->np_pj, c->scal, 1));
+    CHK(d2h_sync(c, beta0, c->scal, 1));
+    c->beta0 = *beta0;
+    return GK_OK;
+}
+
+int gk_zero_x(gk_ctx *c) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    HIPCHK(hipMemsetAsync(c->x, 0, sizeof(double) * c->nloc, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return GK_OK;
+}
+
+int gk_get_x(gk_ctx *c, double *x) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    HIPCHK(hipMemcpyAsync(x, c->x, sizeof(double) * c->nloc, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return GK_OK;
+}
+
+int gk_set_x(gk_ctx *c, const double *x) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    HIPCHK(hipMemcpyAsync(c->x, x, sizeof(double) * c->nloc, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return GK_OK;
+}
+
+int gk_true_residual(gk_ctx *c, double *rel) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    double b0;
+    if (c->beta0 < 0) CHK(gk_rhs_norm(c, &b0));
+    CHK(halo(c, c->x));
+    gk::StArgs a{};
+    a.x = c->x;
+    a.in1 = c->b;
+    a.y = c->aux;
+    a.part = slot(c, 2);
+    CHK(stencil(c, gk::OP_RESID, gk::ACC_NORM, a));
+    CHK(allreduce(c, slot(c, 2), c->np_st));
+    CHK(finalize(c, slot(c, 2), c->np_st, c->scal + 1, 1));
+    double r;
+    CHK(d2h_sync(c, &r, c->scal + 1, 1));
+    *rel = r / c->beta0;
+    return GK_OK;
+}
+
+// ------------------------------------------------------------------ MGS-R --
+
+int gk_mgs_cycle_start(gk_ctx *c, double *beta) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    CHK(op_precond(c, c->x, c->w, true, gk::ACC_NORM, nullptr, slot(c, 0)));
+    CHK(allreduce(c, slot(c, 0), c->np_st));
+    CHK(scale(c, c->V, c->w, slot(c, 0), c->np_st, c->hcol));
+    CHK(d2h_sync(c, beta, c->hcol, 1));
+    c->cycle_mgs = true;
+    c->cycle_hh = false;
+    return GK_OK;
+}
+
+int gk_mgs_step(gk_ctx *c, int j, double *hcol) {
+    CHK(check_ctx(c));
+    if (j < 1 || j > c->m) return set_err(GK_ERR_ARG, "step j=%d outside 1..%d", j, c->m);
+    if (!c->cycle_mgs) return set_err(GK_ERR_STATE, "gk_mgs_step before gk_mgs_cycle_start");
+    HIPCHK(hipSetDevice(c->dev));
+    const i64 ld = c->ld;
+    double *V = c->V;
+    HIPCHK(hipMemsetAsync(c->hcol, 0, sizeof(double) * (j + 1), c->st));
+    int s0 = 0, s1 = 1;
+    // w = M^-1 A V(:,j), fused with the first dot <w, V(:,1)>
+    CHK(op_precond(c, V + (i64)(j - 1) * ld, c->w, false, gk::ACC_DOT, V, slot(c, s0)));
+    int np = c->np_st;
+    // two MGS passes: projection p = (k, i), AXPY of p fused with the dot of p+1
+    const int np_total = 2 * j;
+    for (int p = 0; p < np_total; ++p) {
+        const int i = p % j;
+        CHK(allreduce(c, slot(c, s0), np));
+        const double *va = V + (i64)i * ld;
+        if (p + 1 < np_total) {
+            const double *vb = V + (i64)((p + 1) % j) * ld;
+            CHK(proj(c, gk::PJ_AXPY_DOT, c->w, va, vb, slot(c, s0), np, slot(c, s1), c->hcol + i, 1.0));
+        } else {
+            CHK(proj(c, gk::PJ_AXPY_NORM, c->w, va, nullptr, slot(c, s0), np, slot(c, s1), c->hcol + i, 1.0));
+        }
+        np = c->np_pj;
+        std::swap(s0, s1);
+    }
+    CHK(allreduce(c, slot(c, s0), np));
+    // h = ||w||, V(:,j+1) = w / h
+    CHK(scale(c, V + (i64)j * ld, c->w, slot(c, s0), np, c->hcol + j));
+    CHK(d2h_sync(c, hcol, c->hcol, j + 1));
+    return GK_OK;
+}
+
+int gk_update_x(gk_ctx *c, const double *y, int n_out) {
+    CHK(check_ctx(c));
+    if (n_out < 1 || n_out > c->m) return set_err(GK_ERR_ARG, "bad n_out %d", n_out);
+    HIPCHK(hipSetDevice(c->dev));
+    HIPCHK(hipMemcpyAsync(c->ydev, y, sizeof(double) * n_out, hipMemcpyHostToDevice, c->st));
+    {
+        ProfScope ps(c, GK_KID_UPDATE);
+        gk::k_update_x<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->x, c->V, c->ld, c->ydev, n_out, c->nloc);
+        LAUNCHCHK();
+    }
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (c->prof) CHK(prof_harvest(c));
+    return GK_OK;
+}
+
+int gk_mgs_verr(gk_ctx *c, int n_out, int zero_last, double *v_err) {
+    CHK(check_ctx(c));
+    if (n_out < 1 || n_out > c->m) return set_err(GK_ERR_ARG, "bad n_out %d", n_out);
+    HIPCHK(hipSetDevice(c->dev));
+    const int nc = n_out + 1;
+    std::vector<double> G;
+    CHK(gram(c, c->V, nc, G));
+    if (zero_last)
+        for (int i = 0; i < nc; ++i) {
+            G[(size_t)(nc - 1) * nc + i] = 0.0;
+            G[(size_t)i * nc + nc - 1] = 0.0;
+        }
+    // v_err(j+1) = sqrt(v_err(j)^2 + sum_{i<=j} 2 (V_i.V_{j+1})^2 + (V_{j+1}.V_{j+1}-1)^2)
+    for (int k = 0; k <= c->m; ++k) v_err[k] = 0.0;
+    for (int j = 1; j <= n_out; ++j) {
+        double s = 0.0;
+        for (int i = 1; i <= j; ++i) {
+            const double d = G[(size_t)j * nc + (i - 1)];
+            s = s + 2.0 * (d * d);
+        }
+        const double dd = G[(size_t)j * nc + j] - 1.0;
+        s = s + dd * dd;
+        v_err[j] = std::sqrt(v_err[j - 1] * v_err[j - 1] + s);
+    }
+    return GK_OK;
+}
+
+// ------------------------------------------------------------- Householder --
+
+static int hh_pivot(gk_ctx *c, int j, double *hostout, int nout) {
+    // hb[0..j] = w(1:j+1) from the owning rank, broadcast
+    const int root = owner_of(c, j);
+    if (c->rank == root)
+        HIPCHK(hipMemcpyAsync(c->hb, c->w + (0 - c->g0), sizeof(double) * (j + 1), hipMemcpyDeviceToDevice, c->st));
+    CHK(bcast(c, c->hb, j + 1, root));
+    return GK_OK;
+    (void)hostout;
+    (void)nout;
+}
+
+int gk_hh_cycle_start(gk_ctx *c, int precondition, double *g1) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    if (c->nranks > 1 && c->rank == 0 && c->nloc < c->m + 2)
+        return set_err(GK_ERR_ARG, "Householder path needs the first slab to hold m+2 unknowns");
+    if (precondition) {
+        CHK(op_precond(c, c->x, c->w, true, gk::ACC_NORM, nullptr, slot(c, 0)));
+    } else {
+        CHK(halo(c, c->x));
+        gk::StArgs a{};
+        a.x = c->x;
+        a.in1 = c->b;
+        a.y = c->w;
+        a.part = slot(c, 0);
+        CHK(stencil(c, gk::OP_RESID, gk::ACC_NORM, a));
+    }
+    CHK(allreduce(c, slot(c, 0), c->np_st));
+    CHK(hh_pivot(c, 0, nullptr, 0));
+    {
+        ProfScope ps(c, GK_KID_OTHER);
+        gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, 0), c->np_st, 0, c->hcol, c->scal + 2);
+        LAUNCHCHK();
+        // w(1) = sign(beta,w(1)) + w(1); norm2(w)
+        gk::k_hh_fix<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->w, c->nloc, c->g0, 0, 0, c->scal + 2, slot(c, 1));
+        LAUNCHCHK();
+    }
+    CHK(allreduce(c, slot(c, 1), c->nblk_stream));
+    CHK(scale(c, c->V, c->w, slot(c, 1), c->nblk_stream, nullptr));
+    CHK(d2h_sync(c, g1, c->hcol, 1));
+    c->cycle_hh = true;
+    c->cycle_mgs = false;
+    return GK_OK;
+}
+
+int gk_hh_step(gk_ctx *c, int j, int precondition, double *hcol) {
+    CHK(check_ctx(c));
+    if (j < 1 || j > c->m) return set_err(GK_ERR_ARG, "step j=%d outside 1..%d", j, c->m);
+    if (!c->cycle_hh) return set_err(GK_ERR_STATE, "gk_hh_step before gk_hh_cycle_start");
+    HIPCHK(hipSetDevice(c->dev));
+    const i64 ld = c->ld;
+    double *P = c->V;
+    // v_j = e_j ; v_j = P_1 .. P_j e_j
+    {
+        ProfScope ps(c, GK_KID_OTHER);
+        gk::k_set_unit<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->vj, c->nloc, c->g0, j - 1, 1.0);
+        LAUNCHCHK();
+    }
+    CHK(reflect_chain_down(c, c->vj, j));
+    // w = M^-1 A v_j (or A v_j), fused with <w, P_1>
+    int s0 = 0, s1 = 1;
+    if (precondition) {
+        CHK(op_precond(c, c->vj, c->w, false, gk::ACC_DOT, P, slot(c, s0)));
+    } else {
+        CHK(halo(c, c->vj));
+        gk::StArgs a{};
+        a.x = c->vj;
+        a.y = c->w;
+        a.vdot = P;
+        a.part = slot(c, s0);
+        CHK(stencil(c, gk::OP_PLAIN, gk::ACC_DOT, a));
+    }
+    int np = c->np_st;
+    // w = P_j .. P_1 w ; the last reflection also accumulates ||w(j+1:n)||^2
+    for (int i = 1; i <= j; ++i) {
+        CHK(allreduce(c, slot(c, s0), np));
+        const double *va = P + (i64)(i - 1) * ld;
+        if (i < j) {
+            CHK(proj(c, gk::PJ_AXPY_DOT, c->w, va, P + (i64)i * ld, slot(c, s0), np, slot(c, s1), nullptr, 2.0));
+        } else {
+            CHK(proj(c, gk::PJ_AXPY_NORM, c->w, va, nullptr, slot(c, s0), np, slot(c, s1), nullptr, 2.0,
+                     (i64)j - c->g0));
+        }
+        np = c->np_pj;
+        std::swap(s0, s1);
+    }
+    CHK(allreduce(c, slot(c, s0), np));
+    CHK(hh_pivot(c, j, nullptr, 0));
+    {
+        ProfScope ps(c, GK_KID_OTHER);
+        gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, s0), np, j, c->hcol, c->scal + 2);
+        LAUNCHCHK();
+        gk::k_hh_fix<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->w, c->nloc, c->g0, j, j, c->scal + 2, slot(c, s1));
+        LAUNCHCHK();
+    }
+    CHK(allreduce(c, slot(c, s1), c->nblk_stream));
+    CHK(scale(c, P + (i64)j * ld, c->w, slot(c, s1), c->nblk_stream, nullptr));
+    CHK(d2h_sync(c, hcol, c->hcol, j + 1));
+    return GK_OK;
+}
+
+int gk_hh_update_x(gk_ctx *c, const double *y, int n_out) {
+    CHK(check_ctx(c));
+    if (n_out < 1 || n_out > c->m) return set_err(GK_ERR_ARG, "bad n_out %d", n_out);
+    HIPCHK(hipSetDevice(c->dev));
+    HIPCHK(hipMemcpyAsync(c->ydev, y, sizeof(double) * n_out, hipMemcpyHostToDevice, c->st));
+    {
+        ProfScope ps(c, GK_KID_OTHER);
+        gk::k_set_prefix<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->w, c->nloc, c->g0, c->ydev, 0, n_out);
+        LAUNCHCHK();
+    }
+    CHK(reflect_chain_down(c, c->w, n_out));
+    {
+        ProfScope ps(c, GK_KID_UPDATE);
+        gk::k_add<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->x, c->w, c->nloc);
+        LAUNCHCHK();
+    }
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (c->prof) CHK(prof_harvest(c));
+    return GK_OK;
+}
+
+int gk_hh_verr(gk_ctx *c, int n_out, double *v_err) {
+    CHK(check_ctx(c));
+    if (n_out < 1 || n_out > c->m) return set_err(GK_ERR_ARG, "bad n_out %d", n_out);
+    HIPCHK(hipSetDevice(c->dev));
+    if (c->Vb == nullptr) {
+        if (hipMalloc(&c->Vb, sizeof(double) * (size_t)c->ld * c->m) != hipSuccess)
+            return set_err(GK_ERR_NOMEM, "cannot allocate the verr basis");
+    }
+    for (int i = 1; i <= n_out; ++i) {
+        double *col = c->Vb + (i64)(i - 1) * c->ld;
+        gk::k_set_unit<<<c->nblk_stream, gk::TPB, 0, c->st>>>(col, c->nloc, c->g0, i - 1, 1.0);
+        LAUNCHCHK();
+        CHK(reflect_chain_down(c, col, i));
+    }
+    std::vector<double> G;
+    CHK(gram(c, c->Vb, n_out, G));
+    for (int k = 0; k <= c->m; ++k) v_err[k] = 0.0;
+    for (int i = 2; i <= n_out; ++i) {
+        double s = 0.0;
+        for (int jj = 1; jj < i; ++jj) {
+            const double d = G[(size_t)(i - 1) * n_out + (jj - 1)];
+            s = s + 2.0 * (d * d);
+        }
+        v_err[i - 1] = s;
+    }
+    return GK_OK;
+}
+
+int gk_apply(gk_ctx *c, int what, const double *in, double *out) {
+    CHK(check_ctx(c));
+    if (in == nullptr || out == nullptr || (what != 0 && what != 1)) return set_err(GK_ERR_ARG, "bad gk_apply args");
+    HIPCHK(hipSetDevice(c->dev));
+    c->cycle_mgs = c->cycle_hh = false;  // clobbers the work vectors
+    if (what == 0) {
+        HIPCHK(hipMemcpyAsync(c->vj, in, sizeof(double) * c->nloc, hipMemcpyHostToDevice, c->st));
+        CHK(halo(c, c->vj));
+        gk::StArgs a{};
+        a.x = c->vj;
+        a.y = c->w;
+        CHK(stencil(c, gk::OP_PLAIN, gk::ACC_NONE, a));
+    } else {
+        HIPCHK(hipMemcpyAsync(c->z, in, sizeof(double) * c->nloc, hipMemcpyHostToDevice, c->st));
+        if (c->pkind == GK_PREC_IDENTITY) {
+            HIPCHK(hipMemcpyAsync(c->w, c->z, sizeof(double) * c->nloc, hipMemcpyDeviceToDevice, c->st));
+        } else {
+            CHK(precond_sweeps(c, c->w, gk::ACC_NONE, nullptr, nullptr));
+        }
+    }
+    HIPCHK(hipMemcpyAsync(out, c->w, sizeof(double) * c->nloc, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (c->prof) CHK(prof_harvest(c));
+    return GK_OK;
+}
+
+// ---------------------------------------------------------------- profiling --
+
+int gk_profile_enable(gk_ctx *c, int enable) {
+    CHK(check_ctx(c));
+    if (!enable) CHK(prof_harvest(c));
+    c->prof = enable != 0;
+    return GK_OK;
+}
+
+int gk_profile_reset(gk_ctx *c) {
+    CHK(check_ctx(c));
+    CHK(prof_harvest(c));
+    for (int k = 0; k < GK_NKID; ++k) {
+        c->prof_ms[k] = 0.0;
+        c->prof_n[k] = 0;
+    }
+    return GK_OK;
+}
+
+int gk_profile_read(gk_ctx *c, int kid, double *total_ms, long long *launches) {
+    CHK(check_ctx(c));
+    if (kid < 0 || kid >= GK_NKID) return set_err(GK_ERR_ARG, "bad kernel id");
+    CHK(prof_harvest(c));
+    *total_ms = c->prof_ms[kid];
+    *launches = c->prof_n[kid];
+    return GK_OK;
+}
+
+int gk_sync(gk_ctx *c) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (c->prof) CHK(prof_harvest(c));
+    return GK_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------- stateless kernel API ----
+
+namespace {
+// Device scratch for the stateless calls: NSLOT partial slabs + a scalar area.
+double *g_scratch[64] = {nullptr};
+
+int stateless_ctx(gk_ctx &c, int N, int nlines, i64 n, void *stream) {
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return set_err(GK_ERR_ARG, "device id %d", dev);
+    if (g_scratch[dev] == nullptr) {
+        if (hipMalloc(&g_scratch[dev], sizeof(double) * (NSLOT * gk::NPMAX + 64)) != hipSuccess)
+            return set_err(GK_ERR_NOMEM, "scratch allocation failed");
+    }
+    c.dev = dev;
+    c.N = N;
+    c.nlines = nlines;
+    c.nloc = n;
+    c.max_lines = nlines;
+    c.st = reinterpret_cast<hipStream_t>(stream);
+    c.red = g_scratch[dev];
+    c.scal = g_scratch[dev] + NSLOT * gk::NPMAX;
+    set_geometry(&c);
+    return GK_OK;
+}
+
+void release_stateless(gk_ctx &c) {
+    // nothing owned: keep the destructor-free fields from being freed
+    c.red = nullptr;
+    c.scal = nullptr;
+    c.st = nullptr;
+}
+
+bool aligned16(const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+}  // namespace
+
+extern "C" {
+
+int gk_poisson5(int nside, int nlines, const double *x, const double *hlo, const double *hhi, double *y,
+                void *stream) {
+    if (nside < 2 || nlines < 1 || x == nullptr || y == nullptr) return set_err(GK_ERR_ARG, "bad poisson5 args");
+    if (!aligned16(x) || !aligned16(y) || !aligned16(hlo) || !aligned16(hhi))
+        return set_err(GK_ERR_ARG, "device pointers must be 16-byte aligned");
+    gk_ctx c;
+    CHK(stateless_ctx(c, nside, nlines, (i64)nside * nlines, stream));
+    gk::StArgs a{};
+    a.x = x;
+    a.y = y;
+    a.N = nside;
+    a.nlines = nlines;
+    a.JT = c.JT;
+    a.hlo = hlo;
+    a.hhi = hhi;
+    int rc = (c.vec == 2) ? launch_stencil_v<2, gk::OP_PLAIN, gk::ACC_NONE>(&c, a)
+                          : launch_stencil_v<1, gk::OP_PLAIN, gk::ACC_NONE>(&c, a);
+    release_stateless(c);
+    return rc;
+}
+
+int gk_precond_apply(int nside, int kind, const double *params, int degree, const double *r, double *z,
+                     double *scratch, void *stream) {
+    if (nside < 2 || r == nullptr || z == nullptr) return set_err(GK_ERR_ARG, "bad precond args");
+    if (!aligned16(r) || !aligned16(z) || !aligned16(scratch))
+        return set_err(GK_ERR_ARG, "device pointers must be 16-byte aligned");
+    const i64 n = (i64)nside * nside;
+    gk_ctx c;
+    CHK(stateless_ctx(c, nside, nside, n, stream));
+    int rc = gk_set_precond(&c, kind, params, params ? 2 : 0, degree);
+    if (rc == GK_OK && kind == GK_PREC_IDENTITY) {
+        rc = hipMemcpyAsync(z, r, sizeof(double) * n, hipMemcpyDeviceToDevice, c.st) == hipSuccess
+                 ? GK_OK
+                 : set_err(GK_ERR_HIP, "copy failed");
+    } else if (rc == GK_OK) {
+        if (scratch == nullptr && kind == GK_PREC_CHEB) {
+            rc = set_err(GK_ERR_ARG, "Chebyshev needs 3 scratch vectors");
+        } else {
+            // op_precond expects z = A v already formed for a step; here the input
+            // IS the residual, so run the preconditioner sweeps directly on r.
+            c.z = const_cast<double *>(r);
+            c.aux = scratch;
+            c.dA = scratch ? scratch + n : nullptr;
+            c.dB = scratch ? scratch + 2 * n : nullptr;
+            rc = precond_sweeps(&c, z, gk::ACC_NONE, nullptr, nullptr);
+        }
+    }
+    c.z = c.aux = c.dA = c.dB = nullptr;
+    release_stateless(c);
+    return rc;
+}
+
+int gk_mgs_project(long long n, double *w, const double *va, double *result, void *stream) {
+    if (n < 1 || w == nullptr || va == nullptr || result == nullptr) return set_err(GK_ERR_ARG, "bad args");
+    if (!aligned16(w) || !aligned16(va)) return set_err(GK_ERR_ARG, "device pointers must be 16-byte aligned");
+    gk_ctx c;
+    CHK(stateless_ctx(c, 2, 1, n, stream));
+    int rc = GK_OK;
+    if (hipMemsetAsync(result, 0, sizeof(double), c.st) != hipSuccess) rc = set_err(GK_ERR_HIP, "memset");
+    if (rc == GK_OK) rc = proj(&c, gk::PJ_DOT, w, nullptr, va, nullptr, 0, slot(&c, 0), nullptr, 1.0);
+    if (rc == GK_OK) rc = proj(&c, gk::PJ_AXPY, w, va, nullptr, slot(&c, 0), c.np_pj, nullptr, result, 1.0);
+    release_stateless(c);
+    return rc;
+}
+
+int gk_dot(long long n, const double *a, const double *b, double *result, void *stream) {
+    if (n < 1 || a == nullptr || b == nullptr || result == nullptr) return set_err(GK_ERR_ARG, "bad args");
+    if (!aligned16(a) || !aligned16(b)) return set_err(GK_ERR_ARG, "device pointers must be 16-byte aligned");
+    gk_ctx c;
+    CHK(stateless_ctx(c, 2, 1, n, stream));
+    int rc = proj(&c, gk::PJ_DOT, const_cast<double *>(a), nullptr, b, nullptr, 0, slot(&c, 0), nullptr, 1.0);
+    if (rc == GK_OK) rc = finalize(&c, slot(&c, 0), c.np_pj, result, 0);
+    release_stateless(c);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,506 @@
+// gk_kernels.hpp -- CDNA4 (gfx950) HIP kernels for the GMRES(m) inner cycle.
+//
+// Every kernel is HBM-bandwidth bound (fp64, ~0.1-0.3 flop/B), so the design
+// rules are: 16-byte (double2) coalesced accesses along the fast grid index i,
+// enough independent loads in flight per wave, one pass over each vector per
+// launch, and reductions that never leave the device.  No MFMA: nothing here
+// is GEMM-shaped except the off-metric Gram diagnostic.
+//
+// Reductions are deterministic: every producer writes one partial per
+// workgroup into a fixed-length slab; the consumer kernel (the next launch in
+// the MGS chain) re-reduces the slab in a fixed order in its prologue
+// ("launch-boundary reduce", cdna_hip_programming.md 5, item 2), so a dot
+// product never needs an atomic, a grid barrier or a host round trip, and on
+// N GPUs the slab itself is what RCCL all-reduces.
+//
+// Compiled with -ffp-contract=off: elementwise results are bit-identical to
+// the CPU oracle (same association order as the Fortran reference); only the
+// dot-product summation order differs.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace gk {
+
+constexpr int TPB = 256;          // threads per workgroup (4 wave64)
+constexpr int WAVES = TPB / 64;
+constexpr int UNR = 4;            // double2 per thread per trip in the streaming kernels
+constexpr int NPMAX = 4096;       // max partials in a slab
+
+typedef long long i64;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Deterministic block sum; result returned to every thread.
+__device__ __forceinline__ double block_sum(double v, double *sm) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) sm[wid] = v;
+    __syncthreads();
+    double r = sm[0];
+#pragma unroll
+    for (int k = 1; k < WAVES; ++k) r += sm[k];
+    return r;
+}
+
+// Fixed-order reduction of a partial slab (length np <= NPMAX).
+__device__ __forceinline__ double reduce_slab(const double *__restrict__ p, int np, double *sm) {
+    double s = 0.0;
+    for (int k = threadIdx.x; k < np; k += TPB) s += p[k];
+    return block_sum(s, sm);
+}
+
+// --------------------------------------------------------------------------
+// Projection kernel: the MGS-R / Householder inner cascade
+// (gmres_mgsr.f90:343-358, gmres_hh.f90:269-304).
+//
+//   h    = sum(pin[0..npin))            (the previous launch's dot, reduced)
+//   w   -= (coef*h) * va                (AXPY with the just-finished dot)
+//   acc += w * vb   or   w * w          (the NEXT dot, fused into the same pass)
+//
+// One launch = one AXPY of projection i fused with the dot of projection i+1:
+// reads w, va, vb and writes w (32 B/unknown) where the reference's separate
+// dot + AXPY move 40 B/unknown.
+// --------------------------------------------------------------------------
+enum { PJ_DOT = 0, PJ_AXPY = 1, PJ_AXPY_DOT = 2, PJ_AXPY_NORM = 3 };
+
+template <int MODE>
+__global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const double *__restrict__ va,
+                                              const double *__restrict__ vb,
+                                              const double *__restrict__ pin, int npin,
+                                              double *__restrict__ pout, double *__restrict__ hslot,
+                                              double coef, i64 n, i64 tail0) {
+    __shared__ double sm[WAVES];
+    double ch = 0.0;
+    if (MODE != PJ_DOT) {
+        const double h = reduce_slab(pin, npin, sm);
+        if (hslot != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hslot = *hslot + h;
+        ch = coef * h;
+    }
+    const i64 n2 = n >> 1;
+    double2 *__restrict__ W2 = reinterpret_cast<double2 *>(w);
+    const double2 *__restrict__ A2 = reinterpret_cast<const double2 *>(va);
+    const double2 *__restrict__ B2 = reinterpret_cast<const double2 *>(vb);
+    double acc = 0.0;
+    const i64 stride = (i64)gridDim.x * TPB * UNR;
+    for (i64 base = (i64)blockIdx.x * TPB * UNR + threadIdx.x; base < n2; base += stride) {
+        double2 wv[UNR], av[UNR], bv[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const i64 e = base + (i64)u * TPB;
+            if (e < n2) {
+                wv[u] = W2[e];
+                if (MODE != PJ_DOT) av[u] = A2[e];
+                if (MODE == PJ_DOT || MODE == PJ_AXPY_DOT) bv[u] = B2[e];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const i64 e = base + (i64)u * TPB;
+            if (e < n2) {
+                if (MODE != PJ_DOT) {
+                    wv[u].x = wv[u].x - ch * av[u].x;
+                    wv[u].y = wv[u].y - ch * av[u].y;
+                    W2[e] = wv[u];
+                }
+                if (MODE == PJ_DOT || MODE == PJ_AXPY_DOT) {
+                    acc = acc + wv[u].x * bv[u].x;
+                    acc = acc + wv[u].y * bv[u].y;
+                }
+                if (MODE == PJ_AXPY_NORM) {
+                    if (2 * e >= tail0) acc = acc + wv[u].x * wv[u].x;
+                    if (2 * e + 1 >= tail0) acc = acc + wv[u].y * wv[u].y;
+                }
+            }
+        }
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {  // odd-length tail element
+        const i64 e = n - 1;
+        double x = w[e];
+        if (MODE != PJ_DOT) {
+            x = x - ch * va[e];
+            w[e] = x;
+        }
+        if (MODE == PJ_DOT || MODE == PJ_AXPY_DOT) acc = acc + x * vb[e];
+        if (MODE == PJ_AXPY_NORM && e >= tail0) acc = acc + x * x;
+    }
+    if (MODE != PJ_AXPY) {
+        const double s = block_sum(acc, sm);
+        if (threadIdx.x == 0) pout[blockIdx.x] = s;
+    }
+}
+
+// out = w / h, h = sqrt(sum(pin)) (norm2 + scale, gmres_mgsr.f90:362-363,384).
+// hslot (optional) receives h.  h == 0 (exact breakdown) writes zeros instead
+// of the reference's Inf/NaN.
+__global__ __launch_bounds__(TPB) void k_scale(double *__restrict__ out, const double *__restrict__ w,
+                                               const double *__restrict__ pin, int npin,
+                                               double *__restrict__ hslot, i64 n) {
+    __shared__ double sm[WAVES];
+    const double h = sqrt(reduce_slab(pin, npin, sm));
+    if (hslot != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hslot = h;
+    const i64 n2 = n >> 1;
+    const double2 *__restrict__ W2 = reinterpret_cast<const double2 *>(w);
+    double2 *__restrict__ O2 = reinterpret_cast<double2 *>(out);
+    const i64 stride = (i64)gridDim.x * TPB;
+    if (h != 0.0) {
+        for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n2; e += stride) {
+            double2 v = W2[e];
+            v.x = v.x / h;
+            v.y = v.y / h;
+            O2[e] = v;
+        }
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) out[n - 1] = w[n - 1] / h;
+    } else {
+        for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n2; e += stride) O2[e] = double2{0.0, 0.0};
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) out[n - 1] = 0.0;
+    }
+}
+
+// out[0] = sqrt(sum(pin)) or sum(pin).
+__global__ __launch_bounds__(TPB) void k_finalize(const double *__restrict__ pin, int npin,
+                                                  double *__restrict__ out, int take_sqrt) {
+    __shared__ double sm[WAVES];
+    const double s = reduce_slab(pin, npin, sm);
+    if (threadIdx.x == 0) out[0] = take_sqrt ? sqrt(s) : s;
+}
+
+// x[e] += sum_k V[k*ld + e] * y[k]  (gmres_mgsr.f90:400-406: the reference's
+// row-wise dot_product(V(idx,1:n_out), y) with idx on the lane, k sequential).
+__global__ __launch_bounds__(TPB) void k_update_x(double *__restrict__ x, const double *__restrict__ V,
+                                                  i64 ld, const double *__restrict__ y, int nout, i64 n) {
+    const i64 n2 = n >> 1;
+    const i64 stride = (i64)gridDim.x * TPB;
+    double2 *__restrict__ X2 = reinterpret_cast<double2 *>(x);
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n2; e += stride) {
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < nout; ++k) {
+            const double2 v = reinterpret_cast<const double2 *>(V + (i64)k * ld)[e];
+            const double yk = y[k];
+            s0 = s0 + v.x * yk;
+            s1 = s1 + v.y * yk;
+        }
+        double2 xv = X2[e];
+        xv.x = xv.x + s0;
+        xv.y = xv.y + s1;
+        X2[e] = xv;
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        double s = 0.0;
+        for (int k = 0; k < nout; ++k) s = s + V[(i64)k * ld + n - 1] * y[k];
+        x[n - 1] = x[n - 1] + s;
+    }
+}
+
+// x = x + w  (gmres_hh.f90:374-378)
+__global__ __launch_bounds__(TPB) void k_add(double *__restrict__ x, const double *__restrict__ w, i64 n) {
+    const i64 stride = (i64)gridDim.x * TPB;
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) x[e] = x[e] + w[e];
+}
+
+__global__ __launch_bounds__(TPB) void k_fill(double *__restrict__ x, double v, i64 n) {
+    const i64 stride = (i64)gridDim.x * TPB;
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) x[e] = v;
+}
+
+// x = 0 except x[gk - g0] = vals[k] for global indices gk = k in [0, nvals)
+// (v_j = e_j, gmres_hh.f90:257-265; w(1:n_out) = y, :356-357).
+__global__ __launch_bounds__(TPB) void k_set_prefix(double *__restrict__ x, i64 n, i64 g0,
+                                                    const double *__restrict__ vals, int first,
+                                                    int nvals) {
+    const i64 stride = (i64)gridDim.x * TPB;
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) {
+        const i64 g = g0 + e;
+        x[e] = (g >= first && g < first + nvals) ? vals[g - first] : 0.0;
+    }
+}
+
+// x = e_g (global index g): zero everywhere, `value` at global index g.
+__global__ __launch_bounds__(TPB) void k_set_unit(double *__restrict__ x, i64 n, i64 g0, i64 g, double value) {
+    const i64 stride = (i64)gridDim.x * TPB;
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) x[e] = (g0 + e == g) ? value : 0.0;
+}
+
+// Householder reflector fix-up (gmres_hh.f90:39-41, :305-318): zero global
+// indices < zero_below; at global index fix_idx add delta[0]; accumulate
+// sum w^2 of the result into pout.
+__global__ __launch_bounds__(TPB) void k_hh_fix(double *__restrict__ w, i64 n, i64 g0, i64 zero_below,
+                                                i64 fix_idx, const double *__restrict__ delta,
+                                                double *__restrict__ pout) {
+    __shared__ double sm[WAVES];
+    const i64 stride = (i64)gridDim.x * TPB;
+    const double dl = delta[0];
+    double acc = 0.0;
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) {
+        const i64 g = g0 + e;
+        double v = w[e];
+        if (g < zero_below) {
+            v = 0.0;
+            w[e] = v;
+        } else if (g == fix_idx) {
+            v = v + dl;
+            w[e] = v;
+        }
+        acc = acc + v * v;
+    }
+    const double s = block_sum(acc, sm);
+    if (threadIdx.x == 0) pout[blockIdx.x] = s;
+}
+
+// Householder pivot bookkeeping, one workgroup.  hb[0..j] = w(1:j+1) broadcast
+// from the owning rank; pin = sum of squares of the tail.
+//  start (j == 0): beta = sqrt(sum w^2); g1 = -sign(beta,w1); delta = sign(beta,w1)
+//                  -> res[0] = g1, delta[0] = sign(beta, w1)          (:250-252)
+//  step  (j >= 1): tmp = sqrt(tail); H(j+1,j) = w(j+1) > 0 ? -tmp : tmp
+//                  -> hcol[0..j-1] = w(1:j), hcol[j] = H(j+1,j), delta = -H (:306-316)
+__global__ void k_hh_pivot(const double *__restrict__ hb, const double *__restrict__ pin, int npin,
+                           int j, double *__restrict__ hcol, double *__restrict__ delta) {
+    __shared__ double sm[WAVES];
+    const double s = sqrt(reduce_slab(pin, npin, sm));
+    if (j == 0) {
+        if (threadIdx.x == 0) {
+            const double w1 = hb[0];
+            const double sg = copysign(fabs(s), w1);
+            hcol[0] = -sg;
+            delta[0] = sg;
+        }
+        return;
+    }
+    for (int k = threadIdx.x; k < j; k += blockDim.x) hcol[k] = hb[k];
+    if (threadIdx.x == 0) {
+        const double H = (hb[j] > 0.0) ? -s : s;
+        hcol[j] = H;
+        delta[0] = -H;
+    }
+}
+
+// --------------------------------------------------------------------------
+// Poisson-5 stencil sweep with fused preconditioner epilogues
+// (src/problems/poisson.f90:33-77, src/preconds/chebyshev.f90:27-37).
+//
+// A workgroup owns TPB*VEC consecutive points of the fast index i and marches
+// over JT grid lines j, keeping lines j-1, j, j+1 of the operand in registers:
+// every operand element is read from HBM once (plus one halo line per JT),
+// the W/E neighbours come from the adjacent lanes by __shfl (wave64; lanes 0
+// and 63 read their outer neighbour through L1).  Missing neighbours at the
+// physical boundary are zeros: x + 0 is exact, so the sum ((W+E)+S)+N is
+// bit-identical to the reference's separate edge / corner statements.
+// Lines -1 and nlines come from the halo buffers (RCCL halo exchange on N
+// GPUs) or are zero at the physical boundary.
+// --------------------------------------------------------------------------
+enum {
+    OP_PLAIN = 0,      // y = A x
+    OP_RESID = 1,      // y = b - A x                                (gmres_mgsr.f90:314-319)
+    OP_CBPR2 = 2,      // x = z: zp = z/d, y = zp + alpha*(z - A zp) (chebyshev.f90:27-37)
+    OP_CHEB_FIRST = 3, // x = r: d0 = r/theta; first Chebyshev iteration
+    OP_CHEB_ITER = 4,  // x = d: next Chebyshev iteration
+};
+enum { ACC_NONE = 0, ACC_DOT = 1, ACC_NORM = 2 };
+
+struct StArgs {
+    const double *x;    // operand, nlines*N
+    const double *hlo;  // line -1 (nullptr: physical boundary)
+    const double *hhi;  // line nlines (nullptr: physical boundary)
+    const double *in1;  // RESID: b ; CHEB_ITER: residual r_k
+    const double *in2;  // CHEB_ITER: running sum z_k
+    double *y;          // main output
+    double *o_res;      // CHEB: r_{k+1} (nullptr on the last iteration)
+    double *o_d;        // CHEB: d_{k+1} (nullptr on the last iteration)
+    const double *vdot; // ACC_DOT partner vector
+    double *part;       // partial slab (ACC != NONE)
+    double s1, s2, s3;  // CBPR2: d, alpha ; CHEB: theta(first)/unused, c1, c2
+    int N, nlines, JT;
+};
+
+template <int VEC>
+__device__ __forceinline__ void ld_vec(const double *p, bool ok, double (&v)[VEC]) {
+    if (ok) {
+        if constexpr (VEC == 2) {
+            const double2 t = *reinterpret_cast<const double2 *>(p);
+            v[0] = t.x;
+            v[1] = t.y;
+        } else {
+            v[0] = p[0];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) v[k] = 0.0;
+    }
+}
+
+template <int VEC>
+__device__ __forceinline__ void st_vec(double *p, const double (&v)[VEC]) {
+    if constexpr (VEC == 2) {
+        *reinterpret_cast<double2 *>(p) = double2{v[0], v[1]};
+    } else {
+        p[0] = v[0];
+    }
+}
+
+template <int VEC, int OP, int ACC>
+__global__ __launch_bounds__(TPB) void k_stencil(StArgs a) {
+    __shared__ double sm[WAVES];
+    const int N = a.N;
+    const int lane = threadIdx.x & 63;
+    const i64 i0 = (i64)blockIdx.x * (TPB * VEC) + (i64)VEC * threadIdx.x;
+    const bool act = i0 < N;
+    const int j0 = blockIdx.y * a.JT;
+    const int j1 = min(j0 + a.JT, a.nlines);
+    // operand transform at load (CBPR2: /d ; CHEB_FIRST: /theta)
+    constexpr bool XF = (OP == OP_CBPR2 || OP == OP_CHEB_FIRST);
+    const double dv = a.s1;
+    double acc = 0.0;
+
+    auto line_ptr = [&](int jj) -> const double * {
+        if (jj < 0) return a.hlo;
+        if (jj >= a.nlines) return a.hhi;
+        return a.x + (i64)jj * N;
+    };
+    auto load_line = [&](int jj, double (&raw)[VEC], double (&t)[VEC]) {
+        const double *p = line_ptr(jj);
+        ld_vec<VEC>(p != nullptr ? p + i0 : nullptr, act && p != nullptr, raw);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) t[k] = XF ? raw[k] / dv : raw[k];
+    };
+
+    if (j0 < a.nlines) {
+        double rm[VEC], rc[VEC], rp[VEC], tm[VEC], tc[VEC], tp[VEC];
+        load_line(j0 - 1, rm, tm);
+        load_line(j0, rc, tc);
+        for (int j = j0; j < j1; ++j) {
+            load_line(j + 1, rp, tp);
+            const i64 row = (i64)j * N;
+            // W/E neighbours of the lane's first / last point
+            double left = __shfl_up(tc[VEC - 1], 1, 64);  // previous lane's last point
+            double right = __shfl_down(tc[0], 1, 64);      // next lane's first point
+            if (lane == 0 && act) left = (i0 > 0) ? a.x[row + i0 - 1] : 0.0;
+            if (lane == 63 && act) right = (i0 + VEC < N) ? a.x[row + i0 + VEC] : 0.0;
+            if (XF && lane == 0) left = left / dv;
+            if (XF && lane == 63) right = right / dv;
+            if (i0 == 0) left = 0.0;
+            if (i0 + VEC >= N) right = 0.0;
+            double yv[VEC];
+            double in1v[VEC], in2v[VEC];
+            if (OP == OP_RESID || OP == OP_CHEB_ITER) ld_vec<VEC>(a.in1 + row + i0, act, in1v);
+            if (OP == OP_CHEB_ITER) ld_vec<VEC>(a.in2 + row + i0, act, in2v);
+            double resv[VEC], dnv[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const double W = (k == 0) ? left : tc[k - 1];
+                const double E = (k == VEC - 1) ? right : tc[k + 1];
+                const double s = ((W + E) + tp[k]) + tm[k];
+                const double ax = 4.0 * tc[k] - 1.0 * s;
+                if (OP == OP_PLAIN) {
+                    yv[k] = ax;
+                } else if (OP == OP_RESID) {
+                    yv[k] = in1v[k] - ax;
+                } else if (OP == OP_CBPR2) {
+                    yv[k] = tc[k] + a.s2 * (rc[k] - ax);
+                } else if (OP == OP_CHEB_FIRST) {
+                    // res = r - A d0 ; d1 = c1*d0 + c2*res ; z = d0 + d1
+                    const double res = rc[k] - ax;
+                    const double dn = a.s2 * tc[k] + a.s3 * res;
+                    resv[k] = res;
+                    dnv[k] = dn;
+                    yv[k] = tc[k] + dn;
+                } else {  // OP_CHEB_ITER
+                    const double res = in1v[k] - ax;
+                    const double dn = a.s2 * tc[k] + a.s3 * res;
+                    resv[k] = res;
+                    dnv[k] = dn;
+                    yv[k] = in2v[k] + dn;
+                }
+            }
+            if (act) {
+                st_vec<VEC>(a.y + row + i0, yv);
+                if (OP == OP_CHEB_FIRST || OP == OP_CHEB_ITER) {
+                    if (a.o_res != nullptr) st_vec<VEC>(a.o_res + row + i0, resv);
+                    if (a.o_d != nullptr) st_vec<VEC>(a.o_d + row + i0, dnv);
+                }
+                if (ACC == ACC_DOT) {
+                    double vd[VEC];
+                    ld_vec<VEC>(a.vdot + row + i0, true, vd);
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) acc = acc + yv[k] * vd[k];
+                } else if (ACC == ACC_NORM) {
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) acc = acc + yv[k] * yv[k];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                rm[k] = rc[k];
+                tm[k] = tc[k];
+                rc[k] = rp[k];
+                tc[k] = tp[k];
+            }
+        }
+    }
+    if (ACC != ACC_NONE) {
+        const double s = block_sum(acc, sm);
+        if (threadIdx.x == 0) a.part[(i64)blockIdx.y * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+// --------------------------------------------------------------------------
+// Gram matrix of columns 0..c-1 of V (the v_err diagnostics,
+// gmres_mgsr.f90:414-420, gmres_hh.f90:587-591).  Off the Arnoldi metric.
+// Each workgroup stages GROWS rows x c columns in LDS and accumulates the
+// c(c+1)/2 pairs it owns; slab[blk*npairs + p]; then k_gram_reduce sums the
+// slab over workgroups in a fixed order.
+// --------------------------------------------------------------------------
+constexpr int GROWS = 32;
+constexpr int GCMAX = 128;
+constexpr int GPPT = (GCMAX * (GCMAX + 1) / 2 + TPB - 1) / TPB;  // pairs per thread
+
+__global__ __launch_bounds__(TPB) void k_gram(const double *__restrict__ V, i64 ld, int c, i64 n,
+                                              const short2 *__restrict__ pairs, int npairs,
+                                              double *__restrict__ slab) {
+    __shared__ double tile[GROWS][GCMAX + 1];
+    double acc[GPPT];
+#pragma unroll
+    for (int q = 0; q < GPPT; ++q) acc[q] = 0.0;
+    const i64 nchunks = (n + GROWS - 1) / GROWS;
+    for (i64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        const i64 r0 = ch * GROWS;
+        for (int t = threadIdx.x; t < GROWS * c; t += TPB) {
+            const int col = t / GROWS, r = t % GROWS;
+            const i64 e = r0 + r;
+            tile[r][col] = (e < n) ? V[(i64)col * ld + e] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < GPPT; ++q) {
+            const int p = threadIdx.x + q * TPB;
+            if (p < npairs) {
+                const short2 ab = pairs[p];
+                double s = 0.0;
+#pragma unroll 8
+                for (int r = 0; r < GROWS; ++r) s = s + tile[r][ab.x] * tile[r][ab.y];
+                acc[q] = acc[q] + s;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < GPPT; ++q) {
+        const int p = threadIdx.x + q * TPB;
+        if (p < npairs) slab[(i64)blockIdx.x * npairs + p] = acc[q];
+    }
+}
+
+__global__ __launch_bounds__(TPB) void k_gram_reduce(const double *__restrict__ slab, int nblk, int npairs,
+                                                     double *__restrict__ out) {
+    const int p = blockIdx.x * TPB + threadIdx.x;
+    if (p >= npairs) return;
+    double s = 0.0;
+    for (int b = 0; b < nblk; ++b) s = s + slab[(i64)b * npairs + p];
+    out[p] = s;
+}
+
+}  // namespace gk

@@ -1,0 +1,275 @@
+"""Python-side handle on the MI355X GMRES(m) inner cycle.
+
+The solve loops themselves run in the Fortran host (libgmres_fhost.so:
+gmres_mgsr_hip_run / gmres_hh_hip_run, which mirror gmres_mgsr_omp /
+gmres_mgsr_mf / gmres_hh_omp / gmres_hh_prec_omp of the reference) on top of
+the HIP C-ABI (libgmres_hip.so).  This module only owns the device context
+(one per GPU / rank), sets the right-hand side and the preconditioner, and
+marshals arrays -- the "harness" role the reference's test drivers play
+(tests/test_poisson_mf.f90).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as nat
+
+PREC = {"identity": nat.GK_PREC_IDENTITY, "none": nat.GK_PREC_IDENTITY,
+        "cbpr2": nat.GK_PREC_CBPR2, "cheb": nat.GK_PREC_CHEB, "chebyshev": nat.GK_PREC_CHEB}
+MGSR_MF, MGSR_OMP = 0, 1
+
+
+def _p(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(nat._dp)
+
+
+def slab_partition(N: int, nranks: int) -> list[tuple[int, int]]:
+    """Row-block decomposition over the slow grid index j:
+    rank r owns grid lines [line0_r, line0_r + nlines_r), contiguous, the
+    first N % nranks ranks one line more.  Every rank's slice of every vector
+    (and of every Krylov column) is then contiguous in Fortran order."""
+    if nranks < 1 or nranks > N:
+        raise ValueError(f"cannot split {N} grid lines over {nranks} ranks")
+    base, extra = divmod(N, nranks)
+    out, l0 = [], 0
+    for r in range(nranks):
+        nl = base + (1 if r < extra else 0)
+        out.append((l0, nl))
+        l0 += nl
+    return out
+
+
+@dataclass
+class SolveResult:
+    x: np.ndarray            # local slab of the solution
+    final_err: np.ndarray    # final_err(1:m) of the last cycle
+    v_err: np.ndarray        # v_err(1:m+1)
+    n_out: int
+    cycles_out: int          # restart_out / stages_out
+    n_cycles: int
+    m: int
+    hist_res: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    hist_ferr: np.ndarray = field(default_factory=lambda: np.zeros((0, 0)))
+
+    @property
+    def iterations(self) -> int:
+        """(stages-1)*m + n_out, as tests/test_poisson_mf.f90:47 reports it."""
+        return (self.cycles_out - 1) * self.m + self.n_out
+
+
+class Context:
+    """One device context: a slab of grid lines of an N x N Poisson problem on
+    one GPU, with Krylov dimension m."""
+
+    def __init__(self, N: int, m: int, device: int = 0, line0: int = 0, nlines: int | None = None):
+        self.N, self.m, self.device = int(N), int(m), int(device)
+        self.line0 = int(line0)
+        self.nlines = int(N if nlines is None else nlines)
+        self.nranks, self.rank = 1, 0
+        h = nat.c_vp()
+        nat.check(nat.hip().gk_create(self.device, self.N, self.line0, self.nlines, self.m, ctypes.byref(h)),
+                  "gk_create")
+        self._h = h
+        n = nat.c_ll()
+        nat.check(nat.hip().gk_local_size(self._h, ctypes.byref(n)), "gk_local_size")
+        self.nloc = int(n.value)
+
+    # -- lifetime --------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            nat.hip().gk_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # -- multi-GPU -----------------------------------------------------
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        nat.check(nat.hip().gk_comm_unique_id(buf), "gk_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, max_lines: int, uid: bytes) -> None:
+        assert len(uid) == 128
+        nat.check(nat.hip().gk_comm_init(self._h, nranks, rank, max_lines, uid), "gk_comm_init")
+        self.nranks, self.rank = nranks, rank
+
+    # -- problem setup ---------------------------------------------------
+    def set_precond(self, kind: str | int = "identity", params=(8.2, 0.2), degree: int = 8) -> None:
+        k = PREC[kind] if isinstance(kind, str) else int(kind)
+        pr = np.ascontiguousarray(params, dtype=np.float64)
+        nat.check(nat.hip().gk_set_precond(self._h, k, _p(pr), pr.size, int(degree)), "gk_set_precond")
+
+    def set_rhs(self, b_local: np.ndarray) -> None:
+        b = np.ascontiguousarray(b_local, dtype=np.float64).reshape(-1)
+        assert b.size == self.nloc
+        nat.check(nat.hip().gk_set_rhs(self._h, _p(b)), "gk_set_rhs")
+
+    def set_rhs_ones(self) -> None:
+        """b = A*1, the manufactured RHS of every reference driver."""
+        nat.check(nat.hip().gk_set_rhs_ones(self._h), "gk_set_rhs_ones")
+
+    def rhs_norm(self) -> float:
+        v = ctypes.c_double()
+        nat.check(nat.hip().gk_rhs_norm(self._h, ctypes.byref(v)), "gk_rhs_norm")
+        return v.value
+
+    def get_x(self) -> np.ndarray:
+        x = np.empty(self.nloc)
+        nat.check(nat.hip().gk_get_x(self._h, _p(x)), "gk_get_x")
+        return x
+
+    def set_x(self, x: np.ndarray) -> None:
+        xx = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+        nat.check(nat.hip().gk_set_x(self._h, _p(xx)), "gk_set_x")
+
+    def zero_x(self) -> None:
+        nat.check(nat.hip().gk_zero_x(self._h), "gk_zero_x")
+
+    def apply(self, v: np.ndarray, what: int = 0) -> np.ndarray:
+        """what = 0: A v ; what = 1: M^-1 v (host arrays, local slab)."""
+        vin = np.ascontiguousarray(v, dtype=np.float64).reshape(-1)
+        out = np.empty(self.nloc)
+        nat.check(nat.hip().gk_apply(self._h, what, _p(vin), _p(out)), "gk_apply")
+        return out
+
+    def true_residual(self) -> float:
+        v = ctypes.c_double()
+        nat.check(nat.hip().gk_true_residual(self._h, ctypes.byref(v)), "gk_true_residual")
+        return v.value
+
+    # -- Arnoldi pieces (for tests / custom drivers) -----------------------
+    def mgs_cycle_start(self) -> float:
+        v = ctypes.c_double()
+        nat.check(nat.hip().gk_mgs_cycle_start(self._h, ctypes.byref(v)), "gk_mgs_cycle_start")
+        return v.value
+
+    def mgs_step(self, j: int) -> np.ndarray:
+        h = np.zeros(j + 1)
+        nat.check(nat.hip().gk_mgs_step(self._h, j, _p(h)), "gk_mgs_step")
+        return h
+
+    def update_x(self, y: np.ndarray) -> None:
+        yy = np.ascontiguousarray(y, dtype=np.float64)
+        nat.check(nat.hip().gk_update_x(self._h, _p(yy), yy.size), "gk_update_x")
+
+    # -- profiling -------------------------------------------------------
+    def profile(self, enable: bool = True) -> None:
+        nat.check(nat.hip().gk_profile_enable(self._h, int(enable)), "gk_profile_enable")
+
+    def profile_reset(self) -> None:
+        nat.check(nat.hip().gk_profile_reset(self._h), "gk_profile_reset")
+
+    def profile_read(self) -> dict:
+        out = {}
+        for kid, name in enumerate(nat.KID_NAMES):
+            ms = ctypes.c_double()
+            n = nat.c_ll()
+            nat.check(nat.hip().gk_profile_read(self._h, kid, ctypes.byref(ms), ctypes.byref(n)),
+                      "gk_profile_read")
+            out[name] = (ms.value, int(n.value))
+        return out
+
+    def sync(self) -> None:
+        nat.check(nat.hip().gk_sync(self._h), "gk_sync")
+
+
+def _alloc_hist(m: int, max_cycles: int, want_hist: bool):
+    if want_hist:
+        return np.zeros(max_cycles), np.zeros(max_cycles * m)
+    return np.zeros(1), np.zeros(1)
+
+
+def gmres_mgsr(ctx: Context, tol: float = 1e-15, variant: int = MGSR_OMP, max_cycles: int = 1000,
+               want_verr: bool = True, want_hist: bool = False) -> SolveResult:
+    """Restarted MGS-R GMRES(m) from x0 = 0 (Fortran host loop, HIP vector work).
+    variant MGSR_OMP = gmres_mgsr_omp semantics, MGSR_MF = gmres_mgsr_mf."""
+    m = ctx.m
+    x = np.zeros(ctx.nloc)
+    fe = np.zeros(m)
+    ve = np.zeros(m + 1)
+    n_out, ro, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    hr, hf = _alloc_hist(m, max_cycles, want_hist)
+    st = nat.fhost().gmres_mgsr_hip_run(ctx.handle, m, tol, variant, max_cycles, _p(x), _p(fe), _p(ve),
+                                        ctypes.byref(n_out), ctypes.byref(ro), int(want_verr), int(want_hist),
+                                        _p(hr), _p(hf), ctypes.byref(nc))
+    nat.check(st, "gmres_mgsr_hip_run")
+    r = SolveResult(x=x, final_err=fe, v_err=ve, n_out=n_out.value, cycles_out=ro.value, n_cycles=nc.value, m=m)
+    if want_hist:
+        r.hist_res = hr[: nc.value].copy()
+        r.hist_ferr = hf.reshape(max_cycles, m)[: nc.value].copy()
+    return r
+
+
+def gmres_hh(ctx: Context, tol: float = 1e-15, precondition: bool = False, midcycle_exit: bool | None = None,
+             max_cycles: int = 1000, want_verr: bool = True, want_hist: bool = False) -> SolveResult:
+    """Householder GMRES(m): precondition=False -> gmres_hh_omp (full cycles);
+    precondition=True -> gmres_hh_prec_omp (in-cycle convergence latch)."""
+    if midcycle_exit is None:
+        midcycle_exit = precondition
+    m = ctx.m
+    x = np.zeros(ctx.nloc)
+    fe = np.zeros(m)
+    ve = np.zeros(m + 1)
+    n_out, so, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    hr, hf = _alloc_hist(m, max_cycles, want_hist)
+    st = nat.fhost().gmres_hh_hip_run(ctx.handle, m, tol, int(precondition), int(midcycle_exit), max_cycles,
+                                      _p(x), _p(fe), _p(ve), ctypes.byref(n_out), ctypes.byref(so),
+                                      int(want_verr), int(want_hist), _p(hr), _p(hf), ctypes.byref(nc))
+    nat.check(st, "gmres_hh_hip_run")
+    r = SolveResult(x=x, final_err=fe, v_err=ve, n_out=n_out.value, cycles_out=so.value, n_cycles=nc.value, m=m)
+    if want_hist:
+        r.hist_res = hr[: nc.value].copy()
+        r.hist_ferr = hf.reshape(max_cycles, m)[: nc.value].copy()
+    return r
+
+
+# ---------------------------------------------------------------- kernels ---
+# Stateless kernel-level calls on caller-owned device memory (torch tensors on
+# cuda: plumbing only).  Used by the kernel parity tests.
+
+def _stream_handle(stream) -> int:
+    return int(stream.cuda_stream) if stream is not None else 0
+
+
+def poisson5(x, y, N: int, nlines: int | None = None, halo_lo=None, halo_hi=None, stream=None) -> None:
+    nl = N if nlines is None else nlines
+    nat.check(nat.hip().gk_poisson5(N, nl, x.data_ptr(), halo_lo.data_ptr() if halo_lo is not None else None,
+                                    halo_hi.data_ptr() if halo_hi is not None else None, y.data_ptr(),
+                                    _stream_handle(stream)), "gk_poisson5")
+
+
+def precond_apply(r, z, N: int, kind: str = "cbpr2", params=(8.2, 0.2), degree: int = 8, scratch=None,
+                  stream=None) -> None:
+    pr = np.ascontiguousarray(params, dtype=np.float64)
+    nat.check(nat.hip().gk_precond_apply(N, PREC[kind], _p(pr), degree, r.data_ptr(), z.data_ptr(),
+                                         scratch.data_ptr() if scratch is not None else None,
+                                         _stream_handle(stream)), "gk_precond_apply")
+
+
+def mgs_project(w, va, result, stream=None) -> None:
+    nat.check(nat.hip().gk_mgs_project(w.numel(), w.data_ptr(), va.data_ptr(), result.data_ptr(),
+                                       _stream_handle(stream)), "gk_mgs_project")
+
+
+def dot(a, b, result, stream=None) -> None:
+    nat.check(nat.hip().gk_dot(a.numel(), a.data_ptr(), b.data_ptr(), result.data_ptr(), _stream_handle(stream)),
+              "gk_dot")

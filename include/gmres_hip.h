@@ -1,0 +1,152 @@
+/*
+ * gmres_hip.h -- C-ABI of libgmres_hip.so, the MI355X (gfx950) device side of
+ * the restarted GMRES(m) inner cycle for the 2D Poisson 5-point operator.
+ *
+ * Drop-in boundary.  The reference (AlexanderGSC/gmres, Fortran) plugs its
+ * operator and preconditioner into the solvers through two abstract
+ * interfaces (src/interfaces.f90:13-17 `stencil_vector(x,y,n)` and
+ * :20-27 `precond(A_x,r,z,aux,params,n)`), and the solvers
+ * (src/gmres_mgsr.f90:277-421 gmres_mgsr_omp, :98-199 gmres_mgsr_mf,
+ * src/gmres_hh.f90:211-385 gmres_hh_omp, :388-566 gmres_hh_prec_omp) run the
+ * Arnoldi cycle on host arrays.  This library replaces the vector work of
+ * those solvers with HIP kernels on device-resident data; the small
+ * Hessenberg / Givens / back-solve work stays on the host (Fortran module
+ * gmres_amd/fortran/gmres_hip.f90 binds these symbols with ISO_C_BINDING).
+ *
+ * Conventions
+ *   - Every function returns int status: GK_OK (0) or a negative GK_ERR_*;
+ *     gk_last_error() returns a message for the calling thread's last error.
+ *   - Grid: N x N ("nside"), Fortran column-major, idx = i + (j-1)*N with i
+ *     fastest.  A context owns the slab of grid lines j in [line0, line0+nlines)
+ *     (0-based line0); nloc = N*nlines local unknowns.  Single GPU:
+ *     line0 = 0, nlines = N.
+ *   - Host arrays are plain double* of the local length; device pointers in
+ *     the stateless kernel API are plain device addresses (16-byte aligned).
+ *   - `j` arguments are 1-based Arnoldi step numbers as in the reference.
+ *   - A context is single-host-thread, stream-ordered, not re-entrant.
+ */
+#ifndef GMRES_HIP_H
+#define GMRES_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GK_OK 0
+#define GK_ERR_ARG (-1)   /* bad argument (shape, range, alignment, order) */
+#define GK_ERR_HIP (-2)   /* HIP runtime error */
+#define GK_ERR_RCCL (-3)  /* RCCL error */
+#define GK_ERR_STATE (-4) /* call out of order (e.g. step before cycle start) */
+#define GK_ERR_NOMEM (-5) /* device allocation failed */
+
+/* Preconditioner kinds (the reference's `precond` plug-ins). */
+#define GK_PREC_IDENTITY 0 /* z = r ; config 1 "no precond"  */
+#define GK_PREC_CBPR2 1    /* src/preconds/chebyshev.f90:8-38, params(1:2) */
+#define GK_PREC_CHEB 2     /* Chebyshev(k) semi-iteration, build-defined (BASELINE config 3) */
+
+/* Kernel ids for gk_profile_read(). */
+#define GK_KID_PROJ 0    /* fused MGS-R / Householder projection (axpy_i + dot_{i+1}) */
+#define GK_KID_STENCIL 1 /* Poisson-5 stencil sweeps incl. fused preconditioner sweeps */
+#define GK_KID_SCALE 2   /* normalisation V(:,j+1) = w / h */
+#define GK_KID_UPDATE 3  /* x += V y */
+#define GK_KID_COMM 4    /* RCCL all-reduce / halo / broadcast */
+#define GK_KID_OTHER 5
+#define GK_NKID 6
+
+typedef struct gk_ctx gk_ctx;
+
+const char *gk_last_error(void);
+int gk_version(void);
+
+/* ------------------------------------------------------------ context ---- */
+/* Create a context on HIP device `device` for an N x N grid, owning lines
+ * [line0, line0+nlines), Krylov dimension m (restart length).  Allocates
+ * V (n x (m+1)), the work vectors and the reduction slabs in HBM. */
+int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out);
+int gk_destroy(gk_ctx *ctx);
+/* Multi-GPU: rank 0 calls gk_comm_unique_id, the 128 bytes are shared out of
+ * band, then every rank calls gk_comm_init.  Ranks own consecutive slabs
+ * (rank r-1 below rank r).  `max_lines` = the largest nlines of any rank. */
+int gk_comm_unique_id(unsigned char id[128]);
+int gk_comm_init(gk_ctx *ctx, int nranks, int rank, int max_lines, const unsigned char id[128]);
+int gk_local_size(gk_ctx *ctx, long long *nloc);
+
+/* Preconditioner: kind GK_PREC_*, params (cbpr2: params[0..1] as
+ * chebyshev.f90:19-25; CHEB: interval ends params[0..1]), degree (CHEB only). */
+int gk_set_precond(gk_ctx *ctx, int kind, const double *params, int nparams, int degree);
+/* Right-hand side b (local part, host) or b = A*1 built on device
+ * (the manufactured RHS of every reference driver, test_poisson_mf.f90:39-40). */
+int gk_set_rhs(gk_ctx *ctx, const double *b_local);
+int gk_set_rhs_ones(gk_ctx *ctx);
+/* beta0 = ||b||_2 (global). */
+int gk_rhs_norm(gk_ctx *ctx, double *beta0);
+/* x = 0 (x0 is always 0 in the reference, gmres_mgsr.f90:304). */
+int gk_zero_x(gk_ctx *ctx);
+int gk_get_x(gk_ctx *ctx, double *x_local);
+int gk_set_x(gk_ctx *ctx, const double *x_local);
+/* Host-array operator application on this context's slab (clobbers the
+ * work vectors; not between cycle start and update):  what = 0: out = A in
+ * (stencil_vector, poisson.f90:33-77); what = 1: out = M^-1 in (precond). */
+int gk_apply(gk_ctx *ctx, int what, const double *in, double *out);
+/* ||b - A x|| / ||b|| (global, true unpreconditioned residual). */
+int gk_true_residual(gk_ctx *ctx, double *rel);
+
+/* -------------------------------------------- MGS-R cycle (gmres_mgsr.f90) */
+/* w = M^-1 (b - A x); beta = ||w||; V(:,1) = w / beta   (:314-329).
+ * Returns beta (= g(1)). */
+int gk_mgs_cycle_start(gk_ctx *ctx, double *beta);
+/* Arnoldi step j (1 <= j <= m): z = A V(:,j); w = M^-1 z; two MGS passes
+ * over V(:,1:j) accumulating H(1:j,j); h = ||w||; V(:,j+1) = w / h
+ * (:336-363, :384).  hcol[0..j] = H(1:j+1, j) before any Givens rotation. */
+int gk_mgs_step(gk_ctx *ctx, int j, double *hcol);
+/* x += V(:,1:n_out) y  (:400-406). */
+int gk_update_x(gk_ctx *ctx, const double *y, int n_out);
+/* Orthogonality diagnostic v_err(1:n_out+1) (:414-420) from the Gram matrix
+ * of V(:,1:n_out+1) computed on device.  zero_last != 0 treats V(:,n_out+1)
+ * as the zero column gmres_mgsr_mf leaves after an in-cycle exit (:172-176). */
+int gk_mgs_verr(gk_ctx *ctx, int n_out, int zero_last, double *v_err);
+
+/* -------------------------------------- Householder cycle (gmres_hh.f90) */
+/* Cycle start.  precondition = 0: w = b - A x (gmres_hh_omp :243-253);
+ * 1: w = M^-1 (b - A x) (gmres_hh_prec_omp :425-436).  Builds reflector
+ * P(:,1); returns g1 = g(1) = -sign(beta, w(1)). */
+int gk_hh_cycle_start(gk_ctx *ctx, int precondition, double *g1);
+/* Step j: v = P_1..P_j e_j; w = A v (M^-1 if precondition); w = P_j..P_1 w;
+ * hcol[0..j] = H(1:j+1,j) (H(j+1,j) = -sign(||w(j+1:n)||, w(j+1)));
+ * builds P(:,j+1)  (:255-321 / :438-502). */
+int gk_hh_step(gk_ctx *ctx, int j, int precondition, double *hcol);
+/* x += P_1..P_n_out [y;0]  (:350-378). */
+int gk_hh_update_x(gk_ctx *ctx, const double *y, int n_out);
+/* calculate_verr (:568-593): v_err(i) = sum_{j<i} 2 (V_i.V_j)^2, V rebuilt
+ * from the reflectors on device (extra n x n_out buffer). */
+int gk_hh_verr(gk_ctx *ctx, int n_out, double *v_err);
+
+/* ---------------------------------------------------------- profiling ---- */
+/* When enabled, every launch is bracketed by HIP events on the context
+ * stream; gk_profile_read returns the summed device time (ms) and launch
+ * count per kernel id since the last reset. */
+int gk_profile_enable(gk_ctx *ctx, int enable);
+int gk_profile_reset(gk_ctx *ctx);
+int gk_profile_read(gk_ctx *ctx, int kid, double *total_ms, long long *launches);
+int gk_sync(gk_ctx *ctx);
+
+/* ------------------------- stateless kernel API (caller device memory) ---- */
+/* y = A x on lines [0,nlines) of an N-wide slab; halo_lo / halo_hi are the
+ * grid lines just below / above the slab (NULL at the physical boundary)
+ * -- stencil_vector, src/problems/poisson.f90:33-77.  stream: hipStream_t. */
+int gk_poisson5(int nside, int nlines, const double *x, const double *halo_lo,
+                const double *halo_hi, double *y, void *stream);
+/* z = M^-1 r for the single-slab case (precond, src/interfaces.f90:20-27);
+ * scratch: 3 vectors of N*N doubles. */
+int gk_precond_apply(int nside, int kind, const double *params, int degree, const double *r,
+                     double *z, double *scratch, void *stream);
+/* Fused MGS projection (gmres_mgsr.f90:343-358): h = <w,va>;
+ * w -= h*va; result[0] = h (device). */
+int gk_mgs_project(long long n, double *w, const double *va, double *result, void *stream);
+/* result[0] = <a,b> (device). */
+int gk_dot(long long n, const double *a, const double *b, double *result, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GMRES_HIP_H */

@@ -1,0 +1,164 @@
+"""End-to-end GMRES(m) parity on the GPU (Fortran host + HIP kernels) against
+the CPU oracle and the reference's own recorded outputs (tests/golden).
+
+Tolerance contract (derived from the reference vs itself at 1 vs 8 OpenMP
+threads): per-cycle true residual within rtol 1e-5 / atol 1e-13 on
+the common cycle prefix, iterations to tol within +-1 %, ||x-1||_inf < 1e-9.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "reference_known_answers.json")))
+
+
+def _hist_close(gpu, ref, rtol=1e-5, atol=1e-13):
+    k = min(len(gpu), len(ref))
+    assert k >= 1
+    dev = np.abs(np.asarray(gpu[:k]) - np.asarray(ref[:k]))
+    bad = dev > rtol * np.abs(ref[:k]) + atol
+    assert not bad.any(), f"cycles {np.nonzero(bad)[0].tolist()} deviate: gpu={gpu[:k]} ref={ref[:k]}"
+
+
+def _hist_close_hh(gpu, ref):
+    """Householder tolerance, derived from the reference restatement against
+    itself at 1 vs 8 OpenMP threads (128^2, m=30): 1e-12 relative while
+    r > 1e-6, then up to 1.1e-4 relative (cycles 45-80) and 8e-3 at the 1e-15
+    floor.  Tiers: r > 1e-6 -> rtol 1e-8; r > 1e-12 -> rtol 1e-3; below -> 5e-2."""
+    k = min(len(gpu), len(ref))
+    g, r = np.asarray(gpu[:k]), np.asarray(ref[:k])
+    rtol = np.where(r > 1e-6, 1e-8, np.where(r > 1e-12, 1e-3, 5e-2))
+    bad = np.abs(g - r) > rtol * r + 1e-16
+    assert not bad.any(), f"cycles {np.nonzero(bad)[0].tolist()} deviate"
+
+
+def _solve(N, m, prec="identity", method="mgsr", variant=1, max_cycles=1000, degree=8, want_hist=True):
+    import gmres_amd as ga
+
+    with ga.Context(N, m) as ctx:
+        ctx.set_precond(prec, (8.2, 0.2), degree)
+        ctx.set_rhs_ones()
+        if method == "mgsr":
+            return ga.gmres_mgsr(ctx, 1e-15, variant=variant, max_cycles=max_cycles, want_hist=want_hist)
+        if method == "hh":  # gmres_hh_omp
+            return ga.gmres_hh(ctx, 1e-15, precondition=False, max_cycles=max_cycles, want_hist=want_hist)
+        return ga.gmres_hh(ctx, 1e-15, precondition=True, max_cycles=max_cycles, want_hist=want_hist)
+
+
+def test_mgsr_128_identity_matches_reference(oracle):
+    """Config 1: 128^2, m=30, no preconditioner, to tol 1e-15."""
+    g = GOLD["mgsr_identity_128_m30"]
+    r = _solve(128, 30, "identity")
+    assert abs(r.iterations - g["iterations"]) <= 0.01 * g["iterations"]
+    assert r.final_err[r.n_out - 1] < 1e-15
+    assert np.max(np.abs(r.x - 1.0)) < 1e-9
+    ref = oracle.gmres_mgsr(oracle.rhs_ones(128), 128, 30, variant=oracle.MGSR_OMP)
+    _hist_close(r.hist_res, ref.hist_res)
+    # final_err of the last cycle, step by step
+    k = min(r.n_out, ref.n_out)
+    assert np.allclose(r.final_err[:k], ref.final_err[:k], rtol=1e-2, atol=1e-15)
+
+
+def test_mgsr_128_mf_variant(oracle):
+    r = _solve(128, 30, "identity", variant=0)
+    ref = oracle.gmres_mgsr(oracle.rhs_ones(128), 128, 30, variant=oracle.MGSR_MF)
+    assert abs(r.iterations - ref.iterations) <= 0.01 * ref.iterations
+    _hist_close(r.hist_res, ref.hist_res)
+
+
+def test_mgsr_128_cbpr2_matches_reference(oracle):
+    g = GOLD["mgsr_cbpr2_128_m30"]
+    r = _solve(128, 30, "cbpr2")
+    assert abs(r.iterations - g["iterations"]) <= 0.01 * g["iterations"]
+    assert np.max(np.abs(r.x - 1.0)) < 1e-9
+    ref = oracle.gmres_mgsr(oracle.rhs_ones(128), 128, 30, prec=oracle.PREC_CBPR2, variant=oracle.MGSR_OMP)
+    _hist_close(r.hist_res, ref.hist_res)
+
+
+def test_mgsr_cheb8(oracle):
+    """Chebyshev(8) (build-defined extension of config 3) vs the oracle."""
+    r = _solve(128, 30, "cheb", degree=8)
+    ref = oracle.gmres_mgsr(oracle.rhs_ones(128), 128, 30, prec=oracle.PREC_CHEB, degree=8,
+                            variant=oracle.MGSR_OMP)
+    assert abs(r.iterations - ref.iterations) <= max(1, 0.01 * ref.iterations)
+    _hist_close(r.hist_res, ref.hist_res)
+    assert np.max(np.abs(r.x - 1.0)) < 1e-9
+
+
+def test_hh_128_identity_matches_reference(oracle):
+    g = GOLD["hh_identity_128_m30"]
+    r = _solve(128, 30, method="hh")
+    assert r.iterations == g["iterations"]  # gmres_hh_omp always runs full cycles
+    ref = oracle.gmres_hh(oracle.rhs_ones(128), 128, 30, midcycle_exit=0)
+    _hist_close_hh(r.hist_res, ref.hist_res)
+    assert r.v_err[r.n_out - 1] < 1e-25  # squared metric, reference ~1e-30
+
+
+def test_hh_128_cbpr2_matches_reference(oracle):
+    g = GOLD["hh_cbpr2_128_m30"]
+    r = _solve(128, 30, "cbpr2", method="hh_prec")
+    assert abs(r.iterations - g["iterations"]) <= 0.01 * g["iterations"]
+    ref = oracle.gmres_hh(oracle.rhs_ones(128), 128, 30, prec=oracle.PREC_CBPR2, midcycle_exit=1)
+    _hist_close_hh(r.hist_res, ref.hist_res)
+
+
+@pytest.mark.parametrize("prec,key", [("identity", "mgsr_identity_1024_m95"), ("cbpr2", "mgsr_cbpr2_1024_m95")])
+def test_1024_three_cycles_vs_reference(prec, key):
+    """Config 2 size: the reference's own per-cycle true residuals (serial run)."""
+    g = GOLD[key]
+    r = _solve(1024, 95, prec, max_cycles=3)
+    _hist_close(r.hist_res, g["cycle_true_residual"], rtol=1e-9, atol=0.0)
+
+
+def test_1024_hh_three_cycles_vs_reference():
+    g = GOLD["hh_identity_1024_m95"]
+    r = _solve(1024, 95, method="hh", max_cycles=3)
+    _hist_close(r.hist_res, g["cycle_true_residual"], rtol=1e-9, atol=0.0)
+
+
+def test_mgsr_verr_small(oracle):
+    r = _solve(64, 20, "identity", max_cycles=2)
+    ref = oracle.gmres_mgsr(oracle.rhs_ones(64), 64, 20, variant=oracle.MGSR_OMP, max_cycles=2)
+    # cumulative orthogonality loss: same order of magnitude as the reference
+    a, b = r.v_err[1:r.n_out + 1], ref.v_err[1:ref.n_out + 1]
+    assert np.all(a < 1e-12) and np.all(b < 1e-12)
+
+
+def test_true_residual_and_solution(oracle):
+    import gmres_amd as ga
+
+    N = 96
+    with ga.Context(N, 25) as ctx:
+        ctx.set_rhs_ones()
+        b = ctx.apply(np.ones(N * N), 0)
+        assert np.array_equal(b, oracle.rhs_ones(N))
+        r = ga.gmres_mgsr(ctx, 1e-15, want_hist=True)
+        assert ctx.true_residual() == pytest.approx(r.hist_res[-1], rel=1e-12)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("prec,key", [("identity", "mgsr_identity_4096_m95"), ("cbpr2", "mgsr_cbpr2_4096_m95")])
+def test_4096_first_cycle_vs_reference(prec, key):
+    """North-star size (4096^2, m=95): cycle-1 true residual vs the reference
+    run recorded in the survey (4 significant digits published)."""
+    g = GOLD[key]
+    r = _solve(4096, 95, prec, max_cycles=1, want_hist=True)
+    assert r.hist_res[0] == pytest.approx(g["cycle_true_residual"][0], rel=6e-5)
+
+
+def test_fortran_driver_runs():
+    """The Fortran drop-in driver (tests/test_poisson_mf.f90 CLI) on the GPU."""
+    exe = os.path.join(os.path.dirname(HERE), "gmres_amd", "lib", "test_mfp_hip")
+    out = subprocess.run([exe, "128", "30"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = [l for l in out.stdout.splitlines() if "Iterations until convergence" in l]
+    assert len(lines) == 2
+    its = [int(l.split(":")[1].split()[0]) for l in lines]
+    for it in its:  # HH+cbpr2 and MGSR+cbpr2: 1056 in the reference
+        assert abs(it - 1056) <= 11, out.stdout
