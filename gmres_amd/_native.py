@@ -70,6 +70,7 @@ _SIGS = {
     "gk_profile_reset": (c_int, [c_vp]),
     "gk_profile_read": (c_int, [c_vp, c_int, _dp, ctypes.POINTER(c_ll)]),
     "gk_sync": (c_int, [c_vp]),
+    "gk_set_tuning": (c_int, [c_vp, c_int, c_int]),
     "gk_poisson5": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gk_precond_apply": (c_int, [c_int, c_int, _dp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "gk_mgs_project": (c_int, [c_ll, c_vp, c_vp, c_vp, c_vp]),

@@ -91,6 +91,8 @@ struct gk_ctx {
     int vec = 2, JT = 16;
     dim3 sgrid;
     int np_st = 0, np_pj = 0, nblk_stream = 0;
+    // tuning knobs (gk_set_tuning)
+    int tune_nt = 0, tune_pj_blocks = 0, tune_st_blocks = 0;
     // state
     bool cycle_mgs = false, cycle_hh = false;
     double beta0 = -1.0;
@@ -179,7 +181,8 @@ void set_geometry(gk_ctx *c) {
     const int gx = (N + gk::TPB * c->vec - 1) / (gk::TPB * c->vec);
     const int ml = c->max_lines > 0 ? c->max_lines : c->nlines;
     // ~2048 workgroups for the stencil sweeps, marching JT lines each
-    int JT = (int)std::max<i64>(1, ((i64)ml * gx + 2047) / 2048);
+    const int target = c->tune_st_blocks > 0 ? c->tune_st_blocks : 2048;
+    int JT = (int)std::max<i64>(1, ((i64)ml * gx + target - 1) / target);
     if (JT > 64) JT = 64;
     int gy = (ml + JT - 1) / JT;
     while ((i64)gx * gy > gk::NPMAX) {
@@ -193,6 +196,7 @@ void set_geometry(gk_ctx *c) {
     const i64 nmax2 = ((i64)ml * N + 1) / 2;
     i64 npj = (nmax2 + (i64)gk::TPB * gk::UNR - 1) / ((i64)gk::TPB * gk::UNR);
     if (npj > 2048) npj = 2048;
+    if (c->tune_pj_blocks > 0) npj = std::min<i64>(c->tune_pj_blocks, gk::NPMAX);
     if (npj < 1) npj = 1;
     c->np_pj = (int)npj;
     // elementwise kernels: also from the largest slab (their partial slabs are all-reduced)
@@ -236,25 +240,36 @@ int stencil(gk_ctx *c, int op, int acc, gk::StArgs a) {
     }
 }
 
-int proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
-         int npin, double *pout, double *hslot, double coef, i64 tail0 = 0) {
-    ProfScope ps(c, GK_KID_PROJ);
+template <bool NT>
+void launch_proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
+                 int npin, double *pout, double *hslot, double coef, i64 tail0) {
     const dim3 g(c->np_pj);
     const i64 n = c->nloc;
     switch (mode) {
         case gk::PJ_DOT:
-            gk::k_proj<gk::PJ_DOT><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
+            gk::k_proj<gk::PJ_DOT, NT><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
             break;
         case gk::PJ_AXPY:
-            gk::k_proj<gk::PJ_AXPY><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
+            gk::k_proj<gk::PJ_AXPY, NT><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
             break;
         case gk::PJ_AXPY_DOT:
-            gk::k_proj<gk::PJ_AXPY_DOT><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
+            gk::k_proj<gk::PJ_AXPY_DOT, NT><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n,
+                                                                      tail0);
             break;
         default:
-            gk::k_proj<gk::PJ_AXPY_NORM><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n, tail0);
+            gk::k_proj<gk::PJ_AXPY_NORM, NT><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n,
+                                                                       tail0);
             break;
     }
+}
+
+int proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
+         int npin, double *pout, double *hslot, double coef, i64 tail0 = 0) {
+    ProfScope ps(c, GK_KID_PROJ);
+    if (c->tune_nt)
+        launch_proj<true>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0);
+    else
+        launch_proj<false>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0);
     LAUNCHCHK();
     return GK_OK;
 }
@@ -918,6 +933,18 @@ int gk_apply(gk_ctx *c, int what, const double *in, double *out) {
     HIPCHK(hipMemcpyAsync(out, c->w, sizeof(double) * c->nloc, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     if (c->prof) CHK(prof_harvest(c));
+    return GK_OK;
+}
+
+int gk_set_tuning(gk_ctx *c, int key, int value) {
+    CHK(check_ctx(c));
+    switch (key) {
+        case GK_TUNE_PROJ_NT: c->tune_nt = value != 0; break;
+        case GK_TUNE_PROJ_BLOCKS: c->tune_pj_blocks = value; break;
+        case GK_TUNE_STENCIL_BLOCKS: c->tune_st_blocks = value; break;
+        default: return set_err(GK_ERR_ARG, "unknown tuning key %d", key);
+    }
+    set_geometry(c);
     return GK_OK;
 }
 

@@ -68,7 +68,21 @@ __device__ __forceinline__ double reduce_slab(const double *__restrict__ p, int 
 // --------------------------------------------------------------------------
 enum { PJ_DOT = 0, PJ_AXPY = 1, PJ_AXPY_DOT = 2, PJ_AXPY_NORM = 3 };
 
-template <int MODE>
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+// Load policy for the Krylov-basis columns: plain, or non-temporal (`nt`) so
+// the once-per-launch V stream does not displace w from the Infinity Cache.
+template <bool NT>
+__device__ __forceinline__ double2 ldv(const double2 *p) {
+    if constexpr (NT) {
+        const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
+        return double2{t.x, t.y};
+    } else {
+        return *p;
+    }
+}
+
+template <int MODE, bool NT = false>
 __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const double *__restrict__ va,
                                               const double *__restrict__ vb,
                                               const double *__restrict__ pin, int npin,
@@ -94,8 +108,8 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
             const i64 e = base + (i64)u * TPB;
             if (e < n2) {
                 wv[u] = W2[e];
-                if (MODE != PJ_DOT) av[u] = A2[e];
-                if (MODE == PJ_DOT || MODE == PJ_AXPY_DOT) bv[u] = B2[e];
+                if (MODE != PJ_DOT) av[u] = ldv<NT>(A2 + e);
+                if (MODE == PJ_DOT || MODE == PJ_AXPY_DOT) bv[u] = ldv<NT>(B2 + e);
             }
         }
 #pragma unroll

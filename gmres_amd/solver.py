@@ -188,6 +188,10 @@ class Context:
             out[name] = (ms.value, int(n.value))
         return out
 
+    def tune(self, key: int, value: int) -> None:
+        """Launch-policy knob (include/gmres_hip.h GK_TUNE_*)."""
+        nat.check(nat.hip().gk_set_tuning(self._h, int(key), int(value)), "gk_set_tuning")
+
     def sync(self) -> None:
         nat.check(nat.hip().gk_sync(self._h), "gk_sync")
 

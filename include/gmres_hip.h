@@ -130,6 +130,17 @@ int gk_profile_reset(gk_ctx *ctx);
 int gk_profile_read(gk_ctx *ctx, int kid, double *total_ms, long long *launches);
 int gk_sync(gk_ctx *ctx);
 
+/* Launch-policy knobs (defaults are the tuned values; for A/B measurement).
+ *   GK_TUNE_PROJ_NT        1: non-temporal loads of the Krylov columns in the
+ *                          projection kernel (keeps w resident in the 256 MB
+ *                          Infinity Cache); 0: plain loads
+ *   GK_TUNE_PROJ_BLOCKS    workgroups of the projection kernel (0 = auto)
+ *   GK_TUNE_STENCIL_BLOCKS target workgroups of the stencil sweeps (0 = auto) */
+#define GK_TUNE_PROJ_NT 0
+#define GK_TUNE_PROJ_BLOCKS 1
+#define GK_TUNE_STENCIL_BLOCKS 2
+int gk_set_tuning(gk_ctx *ctx, int key, int value);
+
 /* ------------------------- stateless kernel API (caller device memory) ---- */
 /* y = A x on lines [0,nlines) of an N-wide slab; halo_lo / halo_hi are the
  * grid lines just below / above the slab (NULL at the physical boundary)

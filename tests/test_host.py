@@ -1,0 +1,98 @@
+"""Host-side checks that need no GPU: the C-ABI library and the Fortran host
+library load and export every declared symbol, argument validation fails
+loudly, the slab decomposition is sound."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def built():
+    from gmres_amd import build
+
+    build.build_all()
+    from gmres_amd import _native
+
+    return _native
+
+
+def test_cabi_exports_every_header_symbol(built):
+    L = built.hip()
+    syms = built.header_symbols()
+    assert len(syms) >= 30
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert L.gk_version() >= 1
+
+
+def test_cabi_signatures_cover_header(built):
+    """Every header function has a ctypes signature in _native (and vice versa)."""
+    assert sorted(built._SIGS) == built.header_symbols()
+
+
+def test_fortran_host_exports(built):
+    F = built.fhost()
+    for s in ("gmres_mgsr_hip_run", "gmres_hh_hip_run"):
+        assert hasattr(F, s)
+    out = subprocess.run(["nm", "-D", built.FHOST_SO], capture_output=True, text=True).stdout
+    # the drop-in module procedures exist (Fortran-mangled)
+    for name in ("gmres_mgsr_hip", "gmres_hh_hip", "gmres_hh_prec_hip", "hip_poisson5", "hip_cbpr2"):
+        assert name in out, name
+
+
+def test_cabi_rejects_bad_arguments(built):
+    L = built.hip()
+    h = ctypes.c_void_p()
+    assert L.gk_create(0, 1, 0, 1, 10, ctypes.byref(h)) == -1  # N < 2
+    assert b"bad shape" in L.gk_last_error()
+    assert L.gk_create(0, 16, 10, 10, 10, ctypes.byref(h)) == -1  # slab beyond the grid
+    assert L.gk_mgs_step(None, 1, None) == -1
+    assert L.gk_poisson5(1, 1, None, None, None, None, None) == -1
+
+
+def test_driver_executable_built(built):
+    exe = os.path.join(ROOT, "gmres_amd", "lib", "test_mfp_hip")
+    assert os.access(exe, os.X_OK)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert "usage" in out.stdout
+
+
+def test_slab_partition():
+    from gmres_amd import slab_partition
+
+    for N in (5, 64, 4096, 8192):
+        for R in (1, 2, 3, 4, 7, 8):
+            if R > N:
+                continue
+            parts = slab_partition(N, R)
+            assert parts[0][0] == 0
+            assert sum(nl for _, nl in parts) == N
+            for (a, na), (b, _) in zip(parts, parts[1:]):
+                assert a + na == b
+            assert max(nl for _, nl in parts) - min(nl for _, nl in parts) <= 1
+    with pytest.raises(ValueError):
+        slab_partition(4, 5)
+
+
+def test_no_cpu_fallback_when_library_missing(monkeypatch, tmp_path):
+    """The product path refuses to run without the HIP library."""
+    from gmres_amd import _native
+
+    monkeypatch.setattr(_native, "HIP_SO", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_native, "_hip", None)
+    with pytest.raises(_native.GkError):
+        _native.hip()
+
+
+def test_product_does_not_import_oracle():
+    """Only tests/, __graft_entry__.smoke and bench.py's cpu_baseline may use oracle/."""
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "gmres_amd")):
+        for f in files:
+            if f.endswith((".py", ".hip", ".hpp", ".f90", ".h", ".cpp")):
+                txt = open(os.path.join(dirpath, f)).read()
+                for bad in ("import oracle", "from oracle", "liboracle", "gmres_oracle", "or_gmres", "or_stvec"):
+                    assert bad not in txt, (f, bad)
