@@ -49,6 +49,9 @@ _SIGS = {
     "gk_comm_unique_id": (c_int, [ctypes.c_char_p]),
     "gk_comm_init": (c_int, [c_vp, c_int, c_int, c_int, ctypes.c_char_p]),
     "gk_local_size": (c_int, [c_vp, ctypes.POINTER(c_ll)]),
+    "gk_group_create": (c_int, [c_int, ctypes.POINTER(c_vp)]),
+    "gk_group_destroy": (c_int, [c_vp]),
+    "gk_comm_init_local": (c_int, [c_vp, c_vp, c_int, c_int]),
     "gk_set_precond": (c_int, [c_vp, c_int, _dp, c_int, c_int]),
     "gk_set_rhs": (c_int, [c_vp, _dp]),
     "gk_set_rhs_ones": (c_int, [c_vp]),

@@ -82,12 +82,12 @@ __device__ __forceinline__ double2 ldv(const double2 *p) {
     }
 }
 
-template <int MODE, bool NT = false>
+template <int MODE, bool NT = false, int U = UNR>
 __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const double *__restrict__ va,
                                               const double *__restrict__ vb,
                                               const double *__restrict__ pin, int npin,
                                               double *__restrict__ pout, double *__restrict__ hslot,
-                                              double coef, i64 n, i64 tail0) {
+                                              double coef, i64 n, i64 tail0, int rev, int blocked) {
     __shared__ double sm[WAVES];
     double ch = 0.0;
     if (MODE != PJ_DOT) {
@@ -100,22 +100,43 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
     const double2 *__restrict__ A2 = reinterpret_cast<const double2 *>(va);
     const double2 *__restrict__ B2 = reinterpret_cast<const double2 *>(vb);
     double acc = 0.0;
-    const i64 stride = (i64)gridDim.x * TPB * UNR;
-    for (i64 base = (i64)blockIdx.x * TPB * UNR + threadIdx.x; base < n2; base += stride) {
-        double2 wv[UNR], av[UNR], bv[UNR];
+    // Work mapping: grid-stride over U*TPB double2 chunks (default), or one
+    // contiguous range per workgroup (blocked); rev walks the vector from the
+    // top so the lines the previous launch touched last are reused first
+    // from the Infinity Cache.
+    i64 lo, hi, step;
+    if (blocked) {
+        const i64 chunk = (i64)TPB * U;
+        const i64 per = ((n2 + gridDim.x - 1) / gridDim.x + chunk - 1) / chunk * chunk;
+        lo = (i64)blockIdx.x * per;
+        hi = min(lo + per, n2);
+        step = chunk;
+    } else {
+        lo = (i64)blockIdx.x * TPB * U;
+        hi = n2;
+        step = (i64)gridDim.x * TPB * U;
+    }
+    for (i64 base = lo + threadIdx.x; base < hi; base += step) {
+        double2 wv[U], av[U], bv[U];
+        i64 idx[U];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
+        for (int u = 0; u < U; ++u) {
             const i64 e = base + (i64)u * TPB;
-            if (e < n2) {
+            idx[u] = (e < hi) ? (rev ? n2 - 1 - e : e) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const i64 e = idx[u];
+            if (e >= 0) {
                 wv[u] = W2[e];
                 if (MODE != PJ_DOT) av[u] = ldv<NT>(A2 + e);
                 if (MODE == PJ_DOT || MODE == PJ_AXPY_DOT) bv[u] = ldv<NT>(B2 + e);
             }
         }
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const i64 e = base + (i64)u * TPB;
-            if (e < n2) {
+        for (int u = 0; u < U; ++u) {
+            const i64 e = idx[u];
+            if (e >= 0) {
                 if (MODE != PJ_DOT) {
                     wv[u].x = wv[u].x - ch * av[u].x;
                     wv[u].y = wv[u].y - ch * av[u].y;

@@ -43,6 +43,25 @@ def slab_partition(N: int, nranks: int) -> list[tuple[int, int]]:
     return out
 
 
+class LocalGroup:
+    """In-process communicator (include/gmres_hip.h gk_group): several
+    contexts of one process, one host thread per rank, RCCL's message pattern."""
+
+    def __init__(self, nranks: int):
+        h = nat.c_vp()
+        nat.check(nat.hip().gk_group_create(int(nranks), ctypes.byref(h)), "gk_group_create")
+        self._h, self.nranks = h, int(nranks)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            nat.hip().gk_group_destroy(self._h)
+            self._h = None
+
+
 @dataclass
 class SolveResult:
     x: np.ndarray            # local slab of the solution
@@ -111,6 +130,11 @@ class Context:
         assert len(uid) == 128
         nat.check(nat.hip().gk_comm_init(self._h, nranks, rank, max_lines, uid), "gk_comm_init")
         self.nranks, self.rank = nranks, rank
+
+    def comm_init_local(self, group: "LocalGroup", rank: int, max_lines: int) -> None:
+        nat.check(nat.hip().gk_comm_init_local(self._h, group.handle, rank, max_lines), "gk_comm_init_local")
+        self.nranks, self.rank = group.nranks, rank
+        self._group = group  # keep alive
 
     # -- problem setup ---------------------------------------------------
     def set_precond(self, kind: str | int = "identity", params=(8.2, 0.2), degree: int = 8) -> None:

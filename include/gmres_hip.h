@@ -54,6 +54,7 @@ extern "C" {
 #define GK_NKID 6
 
 typedef struct gk_ctx gk_ctx;
+typedef struct gk_group gk_group;
 
 const char *gk_last_error(void);
 int gk_version(void);
@@ -69,6 +70,12 @@ int gk_destroy(gk_ctx *ctx);
  * (rank r-1 below rank r).  `max_lines` = the largest nlines of any rank. */
 int gk_comm_unique_id(unsigned char id[128]);
 int gk_comm_init(gk_ctx *ctx, int nranks, int rank, int max_lines, const unsigned char id[128]);
+/* In-process communicator with the same message pattern as RCCL: nranks
+ * contexts of ONE process (any devices, e.g. all on one GPU for testing the
+ * slab decomposition), each driven by its own host thread. */
+int gk_group_create(int nranks, gk_group **out);
+int gk_group_destroy(gk_group *g);
+int gk_comm_init_local(gk_ctx *ctx, gk_group *g, int rank, int max_lines);
 int gk_local_size(gk_ctx *ctx, long long *nloc);
 
 /* Preconditioner: kind GK_PREC_*, params (cbpr2: params[0..1] as
@@ -122,9 +129,11 @@ int gk_hh_update_x(gk_ctx *ctx, const double *y, int n_out);
 int gk_hh_verr(gk_ctx *ctx, int n_out, double *v_err);
 
 /* ---------------------------------------------------------- profiling ---- */
-/* When enabled, every launch is bracketed by HIP events on the context
- * stream; gk_profile_read returns the summed device time (ms) and launch
- * count per kernel id since the last reset. */
+/* enable = 1: every launch is bracketed by HIP events on the context stream;
+ * enable = S > 1: only the launches of MGS-R steps with j % S == 0 (launch
+ * durations do not depend on j, so the per-launch average is unbiased while
+ * the event overhead drops S-fold).  gk_profile_read returns the summed
+ * device time (ms) and launch count per kernel id since the last reset. */
 int gk_profile_enable(gk_ctx *ctx, int enable);
 int gk_profile_reset(gk_ctx *ctx);
 int gk_profile_read(gk_ctx *ctx, int kid, double *total_ms, long long *launches);
@@ -133,12 +142,20 @@ int gk_sync(gk_ctx *ctx);
 /* Launch-policy knobs (defaults are the tuned values; for A/B measurement).
  *   GK_TUNE_PROJ_NT        1: non-temporal loads of the Krylov columns in the
  *                          projection kernel (keeps w resident in the 256 MB
- *                          Infinity Cache); 0: plain loads
+ *                          Infinity Cache); 0: plain loads; -1: auto (default:
+ *                          non-temporal when a vector exceeds 48 MiB)
  *   GK_TUNE_PROJ_BLOCKS    workgroups of the projection kernel (0 = auto)
- *   GK_TUNE_STENCIL_BLOCKS target workgroups of the stencil sweeps (0 = auto) */
+ *   GK_TUNE_STENCIL_BLOCKS target workgroups of the stencil sweeps (0 = auto)
+ *   GK_TUNE_PROJ_REV       1: alternate the traversal direction of successive
+ *                          projection launches (Infinity Cache reuse)
+ *   GK_TUNE_PROJ_BLOCKED   1: contiguous range per workgroup; 0: grid-stride
+ *   GK_TUNE_PROJ_UNROLL    double2 loads in flight per thread and array: 2, 4, 8 */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
+#define GK_TUNE_PROJ_REV 3
+#define GK_TUNE_PROJ_BLOCKED 4
+#define GK_TUNE_PROJ_UNROLL 5
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

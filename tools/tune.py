@@ -16,7 +16,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KEYS = {"nt": 0, "pj": 1, "st": 2}
+KEYS = {"nt": 0, "pj": 1, "st": 2, "rev": 3, "blk": 4, "unr": 5}
+DEFAULTS = {0: -1, 1: 0, 2: 0, 3: 0, 4: 0, 5: 2}
 
 
 def parse_variant(s: str) -> dict:
@@ -48,7 +49,7 @@ def main():
     for r in range(a.rounds):
         for v in a.variants:
             for k in KEYS.values():
-                ctx.tune(k, 0)
+                ctx.tune(k, DEFAULTS[k])
             for k, val in parse_variant(v).items():
                 ctx.tune(k, val)
             ctx.sync()
