@@ -108,7 +108,7 @@ def main() -> None:
     ap.add_argument("--cpu-steps", type=int, default=60)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-prof", action="store_true", help="no HIP-event kernel timing in the timed region")
-    ap.add_argument("--prof-every", type=int, default=8,
+    ap.add_argument("--prof-every", type=int, default=16,
                     help="HIP events around the launches of every S-th Arnoldi step (1 = all)")
     args = ap.parse_args()
 

@@ -63,6 +63,8 @@ _SIGS = {
     "gk_true_residual": (c_int, [c_vp, _dp]),
     "gk_mgs_cycle_start": (c_int, [c_vp, _dp]),
     "gk_mgs_step": (c_int, [c_vp, c_int, _dp]),
+    "gk_mgs_step_async": (c_int, [c_vp, c_int]),
+    "gk_mgs_step_wait": (c_int, [c_vp, c_int, _dp]),
     "gk_update_x": (c_int, [c_vp, _dp, c_int]),
     "gk_mgs_verr": (c_int, [c_vp, c_int, c_int, _dp]),
     "gk_hh_cycle_start": (c_int, [c_vp, c_int, _dp]),

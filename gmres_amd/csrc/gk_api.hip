@@ -94,6 +94,10 @@ struct gk_ctx {
     double *hb = nullptr;    // m+2 Householder broadcast buffer
     double *scal = nullptr;  // 8 scalars
     double *hcol_host = nullptr;  // pinned
+    double *hall = nullptr;       // device: per-step Hessenberg columns, m slots of m+2
+    double *hallh = nullptr;      // mapped pinned host mirror of hall (written by k_scale)
+    double *hallh_dev = nullptr;  // its device address
+    std::vector<hipEvent_t> ev_step;  // completion of step j
     double *Vb = nullptr;    // Householder verr basis (lazy)
     double *gram_slab = nullptr, *gram_out = nullptr;
     short2 *gram_pairs = nullptr;
@@ -362,43 +366,43 @@ int stencil(gk_ctx *c, int op, int acc, gk::StArgs a) {
 
 template <bool NT, int U>
 void launch_proj_u(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
-                   int npin, double *pout, double *hslot, double coef, i64 tail0, int rev) {
+                   int npin, double *pout, double *hslot, double coef, i64 tail0, int rev, int hstore) {
     const dim3 g(c->np_pj);
     const i64 n = c->nloc;
     const int bl = c->tune_blocked;
     switch (mode) {
         case gk::PJ_DOT:
             gk::k_proj<gk::PJ_DOT, NT, U><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n,
-                                                                    tail0, rev, bl);
+                                                                    tail0, rev, bl, hstore);
             break;
         case gk::PJ_AXPY:
             gk::k_proj<gk::PJ_AXPY, NT, U><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n,
-                                                                     tail0, rev, bl);
+                                                                     tail0, rev, bl, hstore);
             break;
         case gk::PJ_AXPY_DOT:
             gk::k_proj<gk::PJ_AXPY_DOT, NT, U><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef,
-                                                                         n, tail0, rev, bl);
+                                                                         n, tail0, rev, bl, hstore);
             break;
         default:
             gk::k_proj<gk::PJ_AXPY_NORM, NT, U><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef,
-                                                                          n, tail0, rev, bl);
+                                                                          n, tail0, rev, bl, hstore);
             break;
     }
 }
 
 template <bool NT>
 void launch_proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
-                 int npin, double *pout, double *hslot, double coef, i64 tail0, int rev) {
+                 int npin, double *pout, double *hslot, double coef, i64 tail0, int rev, int hstore) {
     if (c->tune_unr == 2)
-        launch_proj_u<NT, 2>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev);
+        launch_proj_u<NT, 2>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
     else if (c->tune_unr == 8)
-        launch_proj_u<NT, 8>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev);
+        launch_proj_u<NT, 8>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
     else
-        launch_proj_u<NT, 4>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev);
+        launch_proj_u<NT, 4>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
 }
 
 int proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
-         int npin, double *pout, double *hslot, double coef, i64 tail0 = 0) {
+         int npin, double *pout, double *hslot, double coef, i64 tail0 = 0, int hstore = 0) {
     ProfScope ps(c, GK_KID_PROJ);
     int rev = 0;
     if (c->tune_rev) {
@@ -406,16 +410,17 @@ int proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, con
         rev = c->proj_parity;
     }
     if (c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto))
-        launch_proj<true>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev);
+        launch_proj<true>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
     else
-        launch_proj<false>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev);
+        launch_proj<false>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
     LAUNCHCHK();
     return GK_OK;
 }
 
-int scale(gk_ctx *c, double *out, const double *w, const double *pin, int npin, double *hslot) {
+int scale(gk_ctx *c, double *out, const double *w, const double *pin, int npin, double *hslot,
+          double *hcopy = nullptr, const double *hsrc = nullptr, int ncopy = 0) {
     ProfScope ps(c, GK_KID_SCALE);
-    gk::k_scale<<<c->nblk_stream, gk::TPB, 0, c->st>>>(out, w, pin, npin, hslot, c->nloc);
+    gk::k_scale<<<c->nblk_stream, gk::TPB, 0, c->st>>>(out, w, pin, npin, hslot, c->nloc, hcopy, hsrc, ncopy);
     LAUNCHCHK();
     return GK_OK;
 }
@@ -644,6 +649,14 @@ int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out)
         return fail(set_err(GK_ERR_NOMEM, "cannot allocate small buffers"));
     if (hipHostMalloc(&c->hcol_host, sizeof(double) * (m + 2 + gk::GCMAX)) != hipSuccess)
         return fail(set_err(GK_ERR_NOMEM, "cannot allocate pinned buffer"));
+    if (hipMalloc(&c->hall, sizeof(double) * (size_t)(m + 2) * (m + 1)) != hipSuccess ||
+        hipHostMalloc(&c->hallh, sizeof(double) * (size_t)(m + 2) * (m + 1), hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->hallh_dev, c->hallh, 0) != hipSuccess)
+        return fail(set_err(GK_ERR_NOMEM, "cannot allocate the Hessenberg mirrors"));
+    c->ev_step.assign(m + 1, nullptr);
+    for (int k = 0; k <= m; ++k)
+        if (hipEventCreateWithFlags(&c->ev_step[k], hipEventDisableTiming) != hipSuccess)
+            return fail(set_err(GK_ERR_HIP, "event create failed"));
     if (hipMemsetAsync(c->x, 0, vb, c->st) != hipSuccess || hipMemsetAsync(c->b, 0, vb, c->st) != hipSuccess ||
         hipMemsetAsync(c->V, 0, vb * (m + 1), c->st) != hipSuccess ||
         hipMemsetAsync(c->red, 0, sizeof(double) * NSLOT * gk::NPMAX, c->st) != hipSuccess)
@@ -674,6 +687,10 @@ int gk_destroy(gk_ctx *c) {
         if (p) (void)hipFree(p);
     if (c->gram_pairs) (void)hipFree(c->gram_pairs);
     if (c->hcol_host) (void)hipHostFree(c->hcol_host);
+    if (c->hall) (void)hipFree(c->hall);
+    if (c->hallh) (void)hipHostFree(c->hallh);
+    for (hipEvent_t e : c->ev_step)
+        if (e) (void)hipEventDestroy(e);
     for (size_t k = 0; k < c->ev0.size(); ++k) {
         if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
         if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
@@ -860,15 +877,16 @@ int gk_mgs_cycle_start(gk_ctx *c, double *beta) {
     return GK_OK;
 }
 
-int gk_mgs_step(gk_ctx *c, int j, double *hcol) {
+int gk_mgs_step_async(gk_ctx *c, int j) {
     CHK(check_ctx(c));
     if (j < 1 || j > c->m) return set_err(GK_ERR_ARG, "step j=%d outside 1..%d", j, c->m);
     if (!c->cycle_mgs) return set_err(GK_ERR_STATE, "gk_mgs_step before gk_mgs_cycle_start");
     HIPCHK(hipSetDevice(c->dev));
     const i64 ld = c->ld;
     double *V = c->V;
+    const int m2 = c->m + 2;
+    double *hs = c->hall + (i64)(j - 1) * m2;  // H(1:j+1, j) of this step, on device
     c->prof_on_step = (j % c->prof_every) == 0;
-    HIPCHK(hipMemsetAsync(c->hcol, 0, sizeof(double) * (j + 1), c->st));
     int s0 = 0, s1 = 1;
     // w = M^-1 A V(:,j), fused with the first dot <w, V(:,1)>
     CHK(op_precond(c, V + (i64)(j - 1) * ld, c->w, false, gk::ACC_DOT, V, slot(c, s0)));
@@ -879,21 +897,37 @@ int gk_mgs_step(gk_ctx *c, int j, double *hcol) {
         const int i = p % j;
         CHK(allreduce(c, slot(c, s0), np));
         const double *va = V + (i64)i * ld;
+        const int first_pass = p < j;
         if (p + 1 < np_total) {
             const double *vb = V + (i64)((p + 1) % j) * ld;
-            CHK(proj(c, gk::PJ_AXPY_DOT, c->w, va, vb, slot(c, s0), np, slot(c, s1), c->hcol + i, 1.0));
+            CHK(proj(c, gk::PJ_AXPY_DOT, c->w, va, vb, slot(c, s0), np, slot(c, s1), hs + i, 1.0, 0, first_pass));
         } else {
-            CHK(proj(c, gk::PJ_AXPY_NORM, c->w, va, nullptr, slot(c, s0), np, slot(c, s1), c->hcol + i, 1.0));
+            CHK(proj(c, gk::PJ_AXPY_NORM, c->w, va, nullptr, slot(c, s0), np, slot(c, s1), hs + i, 1.0, 0,
+                     first_pass));
         }
         np = c->np_pj;
         std::swap(s0, s1);
     }
     CHK(allreduce(c, slot(c, s0), np));
-    // h = ||w||, V(:,j+1) = w / h
-    CHK(scale(c, V + (i64)j * ld, c->w, slot(c, s0), np, c->hcol + j));
-    CHK(d2h_sync(c, hcol, c->hcol, j + 1));
+    // h = ||w||, V(:,j+1) = w / h; H(1:j+1,j) published to mapped host memory
+    CHK(scale(c, V + (i64)j * ld, c->w, slot(c, s0), np, hs + j, c->hallh_dev + (i64)(j - 1) * m2, hs, j));
+    HIPCHK(hipEventRecord(c->ev_step[j], c->st));
     c->prof_on_step = true;
     return GK_OK;
+}
+
+int gk_mgs_step_wait(gk_ctx *c, int j, double *hcol) {
+    CHK(check_ctx(c));
+    if (j < 1 || j > c->m) return set_err(GK_ERR_ARG, "step j=%d outside 1..%d", j, c->m);
+    HIPCHK(hipEventSynchronize(c->ev_step[j]));
+    const volatile double *src = c->hallh + (i64)(j - 1) * (c->m + 2);
+    for (int k = 0; k <= j; ++k) hcol[k] = src[k];
+    return GK_OK;
+}
+
+int gk_mgs_step(gk_ctx *c, int j, double *hcol) {
+    CHK(gk_mgs_step_async(c, j));
+    return gk_mgs_step_wait(c, j, hcol);
 }
 
 int gk_update_x(gk_ctx *c, const double *y, int n_out) {

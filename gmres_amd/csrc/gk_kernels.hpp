@@ -87,12 +87,14 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
                                               const double *__restrict__ vb,
                                               const double *__restrict__ pin, int npin,
                                               double *__restrict__ pout, double *__restrict__ hslot,
-                                              double coef, i64 n, i64 tail0, int rev, int blocked) {
+                                              double coef, i64 n, i64 tail0, int rev, int blocked,
+                                              int hstore) {
     __shared__ double sm[WAVES];
     double ch = 0.0;
     if (MODE != PJ_DOT) {
         const double h = reduce_slab(pin, npin, sm);
-        if (hslot != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hslot = *hslot + h;
+        // H(i,j) = H(i,j) + h: the first MGS pass starts from H(i,j) = 0
+        if (hslot != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hslot = (hstore ? 0.0 : *hslot) + h;
         ch = coef * h;
     }
     const i64 n2 = n >> 1;
@@ -172,12 +174,20 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
 // out = w / h, h = sqrt(sum(pin)) (norm2 + scale, gmres_mgsr.f90:362-363,384).
 // hslot (optional) receives h.  h == 0 (exact breakdown) writes zeros instead
 // of the reference's Inf/NaN.
+// hcopy (optional): block 0 also publishes hsrc[0..ncopy) and h to hcopy
+// (mapped pinned host memory: the step's Hessenberg column, no extra copy).
 __global__ __launch_bounds__(TPB) void k_scale(double *__restrict__ out, const double *__restrict__ w,
                                                const double *__restrict__ pin, int npin,
-                                               double *__restrict__ hslot, i64 n) {
+                                               double *__restrict__ hslot, i64 n,
+                                               double *__restrict__ hcopy = nullptr,
+                                               const double *__restrict__ hsrc = nullptr, int ncopy = 0) {
     __shared__ double sm[WAVES];
     const double h = sqrt(reduce_slab(pin, npin, sm));
     if (hslot != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hslot = h;
+    if (hcopy != nullptr && blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < ncopy; k += TPB) hcopy[k] = hsrc[k];
+        if (threadIdx.x == 0) hcopy[ncopy] = h;
+    }
     const i64 n2 = n >> 1;
     const double2 *__restrict__ W2 = reinterpret_cast<const double2 *>(w);
     double2 *__restrict__ O2 = reinterpret_cast<double2 *>(out);

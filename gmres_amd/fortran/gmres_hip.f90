@@ -91,6 +91,17 @@ module gmres_hip_c
             integer(c_int), value :: j
             real(c_double), intent(out) :: hcol(*)
         end function
+        integer(c_int) function gk_mgs_step_async(ctx, j) bind(C, name='gk_mgs_step_async')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: j
+        end function
+        integer(c_int) function gk_mgs_step_wait(ctx, j, hcol) bind(C, name='gk_mgs_step_wait')
+            import :: c_int, c_ptr, c_double
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: j
+            real(c_double), intent(out) :: hcol(*)
+        end function
         integer(c_int) function gk_update_x(ctx, y, n_out) bind(C, name='gk_update_x')
             import :: c_int, c_ptr, c_double
             type(c_ptr), value :: ctx
@@ -283,10 +294,18 @@ contains
             st = gk_mgs_cycle_start(ctx, beta); if (st /= GK_OK) return
             g(1) = beta
             exited = .false.
+            ! Pipelined: step j+1 is enqueued on the GPU before the host waits for
+            ! step j's Hessenberg column, so the Givens work below overlaps it.
+            if (.not. converged) then
+                st = gk_mgs_step_async(ctx, 1); if (st /= GK_OK) return
+            end if
             do j = 1, m
                 if (converged) exit
                 n_out = j
-                st = gk_mgs_step(ctx, j, hcol); if (st /= GK_OK) return
+                if (j < m) then
+                    st = gk_mgs_step_async(ctx, j + 1); if (st /= GK_OK) return
+                end if
+                st = gk_mgs_step_wait(ctx, j, hcol); if (st /= GK_OK) return
                 H(1:j + 1, j) = hcol(1:j + 1)
                 h_val = hcol(j + 1)
                 call givens_column(H, cs, sn, g, j)

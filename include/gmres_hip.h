@@ -106,6 +106,13 @@ int gk_mgs_cycle_start(gk_ctx *ctx, double *beta);
  * over V(:,1:j) accumulating H(1:j,j); h = ||w||; V(:,j+1) = w / h
  * (:336-363, :384).  hcol[0..j] = H(1:j+1, j) before any Givens rotation. */
 int gk_mgs_step(gk_ctx *ctx, int j, double *hcol);
+/* The same step split in two so the host can run the Givens rotation of
+ * step j while the GPU already works on step j+1: gk_mgs_step_async enqueues
+ * step j and returns; gk_mgs_step_wait(j) blocks until its Hessenberg column
+ * is available.  Enqueueing step j+1 before step j's convergence test is
+ * harmless: a step only writes w and V(:,j+1) and its own column slot. */
+int gk_mgs_step_async(gk_ctx *ctx, int j);
+int gk_mgs_step_wait(gk_ctx *ctx, int j, double *hcol);
 /* x += V(:,1:n_out) y  (:400-406). */
 int gk_update_x(gk_ctx *ctx, const double *y, int n_out);
 /* Orthogonality diagnostic v_err(1:n_out+1) (:414-420) from the Gram matrix
