@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate passes,
+MI355X_MICROARCH.md §HBM) into profiles/pmc_traffic.json, which bench.py
+quotes as roofline.traffic for the matching workload.
+
+gfx950 corrections applied (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half
+the bytes of a wide coalesced streaming read -> x2; WRITE_SIZE is exact for
+16-B-per-lane streaming stores.  Both derive from the L2's memory-side
+requests, so Infinity-Cache hits are included: the figure is L2<->fabric
+traffic (an upper bound on HBM traffic).
+
+  python tools/pmc_summary.py --fetch F.csv --write W.csv --grid 4096 --m 95 \
+      --prec identity --method mgsr --gpus 1 --kernel "gk::k_proj<2"
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+
+def per_launch(path, kernel):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    return statistics.median(vals) * 1024.0, len(vals)  # counters are in KB
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--grid", type=int, default=4096)
+    ap.add_argument("--m", type=int, default=95)
+    ap.add_argument("--prec", default="identity")
+    ap.add_argument("--method", default="mgsr")
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--kernel", default="gk::k_proj<2")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "profiles", "pmc_traffic.json"))
+    a = ap.parse_args()
+    f, nf = per_launch(a.fetch, a.kernel)
+    w, nw = per_launch(a.write, a.kernel)
+    n = a.grid * a.grid // a.gpus
+    entry = {"kernel": a.kernel, "launches_sampled": [nf, nw],
+             "fetch_bytes_raw": f, "fetch_bytes_corrected": 2 * f, "write_bytes": w,
+             "hbm_bytes_per_launch": 2 * f + w, "bytes_per_unknown": (2 * f + w) / n,
+             "source": f"{os.path.relpath(a.fetch)} + {os.path.relpath(a.write)} (median per launch, "
+                       "FETCH_SIZE x2 gfx950 correction; L2<->fabric bytes incl. Infinity-Cache hits)"}
+    db = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    db[f"{a.grid}_{a.m}_{a.prec}_{a.method}_{a.gpus}"] = entry
+    json.dump(db, open(a.out, "w"), indent=1)
+    print(json.dumps(entry, indent=1))
+
+
+if __name__ == "__main__":
+    main()
