@@ -119,7 +119,7 @@ struct gk_ctx {
     // tuning knobs (gk_set_tuning)
     int tune_nt = -1, tune_pj_blocks = 0, tune_st_blocks = 0;  // tune_nt: -1 auto
     bool nt_auto = false;
-    int tune_rev = 0, tune_blocked = 0, tune_unr = 2, proj_parity = 0;
+    int tune_rev = 0, tune_blocked = 0, tune_unr = 0, proj_parity = 0;  // tune_unr 0 = auto
     int prof_every = 1;       // record events in steps with j % prof_every == 0
     bool prof_on_step = true;
     // state
@@ -393,9 +393,14 @@ void launch_proj_u(gk_ctx *c, int mode, double *w, const double *va, const doubl
 template <bool NT>
 void launch_proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
                  int npin, double *pout, double *hslot, double coef, i64 tail0, int rev, int hstore) {
-    if (c->tune_unr == 2)
+    int u = c->tune_unr;
+    if (u == 0) {  // auto: one trip per thread when the vector is small, else 2 in flight
+        const i64 per_thread = (c->nloc / 2 + (i64)c->np_pj * gk::TPB - 1) / ((i64)c->np_pj * gk::TPB);
+        u = per_thread <= 4 ? 4 : 2;
+    }
+    if (u == 2)
         launch_proj_u<NT, 2>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
-    else if (c->tune_unr == 8)
+    else if (u == 8)
         launch_proj_u<NT, 8>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
     else
         launch_proj_u<NT, 4>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
@@ -1159,7 +1164,8 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_PROJ_REV: c->tune_rev = value != 0; break;
         case GK_TUNE_PROJ_BLOCKED: c->tune_blocked = value != 0; break;
         case GK_TUNE_PROJ_UNROLL:
-            if (value != 2 && value != 4 && value != 8) return set_err(GK_ERR_ARG, "unroll must be 2, 4 or 8");
+            if (value != 0 && value != 2 && value != 4 && value != 8)
+                return set_err(GK_ERR_ARG, "unroll must be 0 (auto), 2, 4 or 8");
             c->tune_unr = value;
             break;
         default: return set_err(GK_ERR_ARG, "unknown tuning key %d", key);

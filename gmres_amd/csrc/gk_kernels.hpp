@@ -90,18 +90,10 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
                                               double coef, i64 n, i64 tail0, int rev, int blocked,
                                               int hstore) {
     __shared__ double sm[WAVES];
-    double ch = 0.0;
-    if (MODE != PJ_DOT) {
-        const double h = reduce_slab(pin, npin, sm);
-        // H(i,j) = H(i,j) + h: the first MGS pass starts from H(i,j) = 0
-        if (hslot != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hslot = (hstore ? 0.0 : *hslot) + h;
-        ch = coef * h;
-    }
     const i64 n2 = n >> 1;
     double2 *__restrict__ W2 = reinterpret_cast<double2 *>(w);
     const double2 *__restrict__ A2 = reinterpret_cast<const double2 *>(va);
     const double2 *__restrict__ B2 = reinterpret_cast<const double2 *>(vb);
-    double acc = 0.0;
     // Work mapping: grid-stride over U*TPB double2 chunks (default), or one
     // contiguous range per workgroup (blocked); rev walks the vector from the
     // top so the lines the previous launch touched last are reused first
@@ -118,9 +110,9 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
         hi = n2;
         step = (i64)gridDim.x * TPB * U;
     }
-    for (i64 base = lo + threadIdx.x; base < hi; base += step) {
-        double2 wv[U], av[U], bv[U];
-        i64 idx[U];
+    double2 wv[U], av[U], bv[U];
+    i64 idx[U];
+    auto issue = [&](i64 base) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const i64 e = base + (i64)u * TPB;
@@ -135,6 +127,21 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
                 if (MODE == PJ_DOT || MODE == PJ_AXPY_DOT) bv[u] = ldv<NT>(B2 + e);
             }
         }
+    };
+    // The first chunk's loads do not depend on h: issue them before the
+    // slab-reduce prologue so their latency hides behind it (matters when a
+    // launch is only a few microseconds: small grids, many GPUs).
+    i64 base = lo + threadIdx.x;
+    if (base < hi) issue(base);
+    double ch = 0.0;
+    if (MODE != PJ_DOT) {
+        const double h = reduce_slab(pin, npin, sm);
+        // H(i,j) = H(i,j) + h: the first MGS pass starts from H(i,j) = 0
+        if (hslot != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hslot = (hstore ? 0.0 : *hslot) + h;
+        ch = coef * h;
+    }
+    double acc = 0.0;
+    while (base < hi) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const i64 e = idx[u];
@@ -154,6 +161,8 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
                 }
             }
         }
+        base += step;
+        if (base < hi) issue(base);
     }
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {  // odd-length tail element
         const i64 e = n - 1;

@@ -156,7 +156,7 @@ int gk_sync(gk_ctx *ctx);
  *   GK_TUNE_PROJ_REV       1: alternate the traversal direction of successive
  *                          projection launches (Infinity Cache reuse)
  *   GK_TUNE_PROJ_BLOCKED   1: contiguous range per workgroup; 0: grid-stride
- *   GK_TUNE_PROJ_UNROLL    double2 loads in flight per thread and array: 2, 4, 8 */
+ *   GK_TUNE_PROJ_UNROLL    double2 loads in flight per thread and array: 2, 4, 8; 0 = auto */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 KEYS = {"nt": 0, "pj": 1, "st": 2, "rev": 3, "blk": 4, "unr": 5}
-DEFAULTS = {0: -1, 1: 0, 2: 0, 3: 0, 4: 0, 5: 2}
+DEFAULTS = {0: -1, 1: 0, 2: 0, 3: 0, 4: 0, 5: 0}
 
 
 def parse_variant(s: str) -> dict:
