@@ -131,9 +131,10 @@ def main() -> None:
     parts = ga.slab_partition(N, world)
     line0, nlines = parts[rank]
     ctx = ga.Context(N, m, device=local, line0=line0, nlines=nlines)
-    if world > 1:
+    if world > 1 or os.environ.get("GK_FORCE_RCCL") == "1":  # 1-rank RCCL: exercises the comm path
         obj = [ga.Context.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
+        if dist is not None:
+            dist.broadcast_object_list(obj, src=0)
         ctx.comm_init(world, rank, max(p[1] for p in parts), obj[0])
     ctx.set_precond(args.prec, (8.2, 0.2), args.degree)
     ctx.set_rhs_ones()

@@ -69,6 +69,8 @@ _SIGS = {
     "gk_mgs_verr": (c_int, [c_vp, c_int, c_int, _dp]),
     "gk_hh_cycle_start": (c_int, [c_vp, c_int, _dp]),
     "gk_hh_step": (c_int, [c_vp, c_int, c_int, _dp]),
+    "gk_hh_step_async": (c_int, [c_vp, c_int, c_int]),
+    "gk_hh_step_wait": (c_int, [c_vp, c_int, _dp]),
     "gk_hh_update_x": (c_int, [c_vp, _dp, c_int]),
     "gk_hh_verr": (c_int, [c_vp, c_int, _dp]),
     "gk_profile_enable": (c_int, [c_vp, c_int]),
@@ -76,6 +78,11 @@ _SIGS = {
     "gk_profile_read": (c_int, [c_vp, c_int, _dp, ctypes.POINTER(c_ll)]),
     "gk_sync": (c_int, [c_vp]),
     "gk_set_tuning": (c_int, [c_vp, c_int, c_int]),
+    "gk_lanczos_bounds": (c_int, [c_vp, c_int, _dp, _dp]),
+    "gk_vec_count": (c_int, [c_vp, _ip]),
+    "gk_vec_apply": (c_int, [c_vp, c_int, c_int, c_int]),
+    "gk_vec_dot": (c_int, [c_vp, c_int, c_int, _dp]),
+    "gk_vec_lincomb": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_double, c_double]),
     "gk_poisson5": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gk_precond_apply": (c_int, [c_int, c_int, _dp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "gk_mgs_project": (c_int, [c_ll, c_vp, c_vp, c_vp, c_vp]),
@@ -83,6 +90,8 @@ _SIGS = {
 }
 
 _FSIGS = {
+    "pcg_hip_run": (c_int, [c_vp, c_double, _ip, _dp, c_int, _dp]),
+    "pbicgstab_hip_run": (c_int, [c_vp, c_double, _ip, _dp, c_int, _dp]),
     "gmres_mgsr_hip_run": (c_int, [c_vp, c_int, c_double, c_int, c_int, _dp, _dp, _dp, _ip, _ip, c_int, c_int,
                                    _dp, _dp, _ip]),
     "gmres_hh_hip_run": (c_int, [c_vp, c_int, c_double, c_int, c_int, c_int, _dp, _dp, _dp, _ip, _ip, c_int,

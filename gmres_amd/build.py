@@ -3,6 +3,7 @@
   gmres_amd/lib/libgmres_hip.so     HIP kernels + C-ABI (include/gmres_hip.h), hipcc
   gmres_amd/lib/libgmres_fhost.so   Fortran host (restart loop, Givens), amdflang
   gmres_amd/lib/test_mfp_hip        Fortran driver mirroring tests/test_poisson_mf.f90
+  gmres_amd/lib/sweep_hip           Fortran sweep drivers (utils.f90 table layout)
 
 hipcc cross-compiles gfx950 code objects without a GPU, so this runs in the
 build container; the .so files travel to the GPU box with the repo snapshot.
@@ -73,10 +74,11 @@ def build_fortran(force: bool = False) -> str:
     link = [f"-L{LIB}", "-lgmres_hip", "-Wl,-rpath,$ORIGIN"]
     if force or _newer(FHOST_SO, F_SOURCES + [HIP_SO]):
         _run([flang(), *common, "-shared", *F_SOURCES, "-o", FHOST_SO, *link])
-    drv_src = os.path.join(FSRC, "test_mfp_hip.f90")
-    if force or _newer(DRIVER, [drv_src, FHOST_SO]):
-        _run([flang(), *common, drv_src, "-o", DRIVER, f"-L{LIB}", "-lgmres_fhost", "-lgmres_hip",
-              "-Wl,-rpath,$ORIGIN"])
+    for name in ("test_mfp_hip", "sweep_hip"):
+        src = os.path.join(FSRC, name + ".f90")
+        exe = os.path.join(LIB, name)
+        if force or _newer(exe, [src, FHOST_SO]):
+            _run([flang(), *common, src, "-o", exe, f"-L{LIB}", "-lgmres_fhost", "-lgmres_hip", "-Wl,-rpath,$ORIGIN"])
     return FHOST_SO
 
 

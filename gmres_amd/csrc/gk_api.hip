@@ -14,6 +14,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdarg>
+#include <cstdlib>
 #include <mutex>
 #include <cstdio>
 #include <cstring>
@@ -181,6 +182,9 @@ __global__ void k_sum_ranks(RankPtrs src, int nr, double *__restrict__ out, int 
     }
 }
 
+// Collectives run whenever a communicator exists (also a 1-rank RCCL one).
+bool collective(const gk_ctx *c) { return c->comm != nullptr || c->lg != nullptr; }
+
 int lg_barrier(gk_ctx *c) {
     gk_group *g = c->lg;
     std::unique_lock<std::mutex> lk(g->mu);
@@ -214,7 +218,7 @@ int lg_wait(gk_ctx *c, int q, bool second) {
 }
 
 int allreduce(gk_ctx *c, double *buf, int count) {
-    if (c->nranks == 1) return GK_OK;
+    if (!collective(c)) return GK_OK;
     ProfScope ps(c, GK_KID_COMM);
     if (c->lg == nullptr) {
         NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->st));
@@ -237,7 +241,7 @@ int allreduce(gk_ctx *c, double *buf, int count) {
 }
 
 int bcast(gk_ctx *c, double *buf, int count, int root) {
-    if (c->nranks == 1) return GK_OK;
+    if (!collective(c)) return GK_OK;
     ProfScope ps(c, GK_KID_COMM);
     if (c->lg == nullptr) {
         NCCLCHK(ncclBroadcast(buf, buf, count, ncclDouble, root, c->comm, c->st));
@@ -257,7 +261,7 @@ int bcast(gk_ctx *c, double *buf, int count, int root) {
 
 // Exchange the first / last local grid line of vec with the slab neighbours.
 int halo(gk_ctx *c, const double *vec) {
-    if (c->nranks == 1) return GK_OK;
+    if (!collective(c)) return GK_OK;
     ProfScope ps(c, GK_KID_COMM);
     const int N = c->N;
     if (c->lg == nullptr) {
@@ -721,7 +725,10 @@ int gk_comm_init(gk_ctx *c, int nranks, int rank, int max_lines, const unsigned 
     c->rank = rank;
     c->max_lines = max_lines;
     set_geometry(c);
-    if (nranks > 1) {
+    // A 1-rank RCCL communicator is only built on request (GK_FORCE_RCCL=1): it
+    // routes every collective through RCCL on one GPU (used by the tests).
+    const char *force = std::getenv("GK_FORCE_RCCL");
+    if (nranks > 1 || (force != nullptr && force[0] == '1')) {
         ncclUniqueId u;
         std::memcpy(&u, id, 128);
         NCCLCHK(ncclCommInitRank(&c->comm, nranks, u, rank));
@@ -1024,7 +1031,7 @@ int gk_hh_cycle_start(gk_ctx *c, int precondition, double *g1) {
     return GK_OK;
 }
 
-int gk_hh_step(gk_ctx *c, int j, int precondition, double *hcol) {
+int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
     CHK(check_ctx(c));
     if (j < 1 || j > c->m) return set_err(GK_ERR_ARG, "step j=%d outside 1..%d", j, c->m);
     if (!c->cycle_hh) return set_err(GK_ERR_STATE, "gk_hh_step before gk_hh_cycle_start");
@@ -1069,15 +1076,26 @@ int gk_hh_step(gk_ctx *c, int j, int precondition, double *hcol) {
     CHK(hh_pivot(c, j, nullptr, 0));
     {
         ProfScope ps(c, GK_KID_OTHER);
-        gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, s0), np, j, c->hcol, c->scal + 2);
+        const int m2 = c->m + 2;
+        gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, s0), np, j, c->hall + (i64)(j - 1) * m2,
+                                                 c->scal + 2, c->hallh_dev + (i64)(j - 1) * m2);
         LAUNCHCHK();
         gk::k_hh_fix<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->w, c->nloc, c->g0, j, j, c->scal + 2, slot(c, s1));
         LAUNCHCHK();
     }
     CHK(allreduce(c, slot(c, s1), c->nblk_stream));
     CHK(scale(c, P + (i64)j * ld, c->w, slot(c, s1), c->nblk_stream, nullptr));
-    CHK(d2h_sync(c, hcol, c->hcol, j + 1));
+    HIPCHK(hipEventRecord(c->ev_step[j], c->st));
     return GK_OK;
+}
+
+int gk_hh_step_wait(gk_ctx *c, int j, double *hcol) {
+    return gk_mgs_step_wait(c, j, hcol);  // same per-step slot + event protocol
+}
+
+int gk_hh_step(gk_ctx *c, int j, int precondition, double *hcol) {
+    CHK(gk_hh_step_async(c, j, precondition));
+    return gk_hh_step_wait(c, j, hcol);
 }
 
 int gk_hh_update_x(gk_ctx *c, const double *y, int n_out) {
@@ -1326,6 +1344,161 @@ int gk_dot(long long n, const double *a, const double *b, double *result, void *
     if (rc == GK_OK) rc = finalize(&c, slot(&c, 0), c.np_pj, result, 0);
     release_stateless(c);
     return rc;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ Lanczos --
+
+namespace {
+// Number of eigenvalues of the symmetric tridiagonal (a, b) smaller than x (Sturm count).
+int sturm_count(const std::vector<double> &a, const std::vector<double> &b, double x) {
+    int cnt = 0;
+    double q = 1.0;
+    for (size_t i = 0; i < a.size(); ++i) {
+        const double bb = i ? b[i - 1] * b[i - 1] : 0.0;
+        q = a[i] - x - (i ? bb / q : 0.0);
+        if (q == 0.0) q = -1e-300;
+        if (q < 0.0) ++cnt;
+    }
+    return cnt;
+}
+
+double tridiag_eig(const std::vector<double> &a, const std::vector<double> &b, int which) {
+    double lo = a[0], hi = a[0];
+    for (size_t i = 0; i < a.size(); ++i) {
+        const double r = (i ? std::fabs(b[i - 1]) : 0.0) + (i + 1 < a.size() ? std::fabs(b[i]) : 0.0);
+        lo = std::min(lo, a[i] - r);
+        hi = std::max(hi, a[i] + r);
+    }
+    for (int it = 0; it < 200; ++it) {  // bisection on the Sturm count
+        const double mid = 0.5 * (lo + hi);
+        if (sturm_count(a, b, mid) > which) hi = mid; else lo = mid;
+    }
+    return 0.5 * (lo + hi);
+}
+
+int dot_host(gk_ctx *c, const double *a, const double *b, double *out) {
+    CHK(proj(c, gk::PJ_DOT, const_cast<double *>(a), nullptr, b, nullptr, 0, slot(c, 3), nullptr, 1.0));
+    CHK(allreduce(c, slot(c, 3), c->np_pj));
+    CHK(finalize(c, slot(c, 3), c->np_pj, c->scal + 6, 0));
+    return d2h_sync(c, out, c->scal + 6, 1);
+}
+
+int axpy_host(gk_ctx *c, double *y, double a, const double *x) {
+    gk::k_axpy_host<<<c->nblk_stream, gk::TPB, 0, c->st>>>(y, a, x, c->nloc);
+    LAUNCHCHK();
+    return GK_OK;
+}
+}  // namespace
+
+extern "C" int gk_lanczos_bounds(gk_ctx *c, int k, double *lmin, double *lmax) {
+    CHK(check_ctx(c));
+    if (k < 2 || k > 1000 || lmin == nullptr || lmax == nullptr) return set_err(GK_ERR_ARG, "bad Lanczos args");
+    HIPCHK(hipSetDevice(c->dev));
+    c->cycle_mgs = c->cycle_hh = false;  // uses the work vectors
+    double *qprev = c->dA, *q = c->dB, *w = c->vj;
+    gk::k_fill_hash<<<c->nblk_stream, gk::TPB, 0, c->st>>>(q, c->nloc, c->g0, 12345ull);
+    LAUNCHCHK();
+    HIPCHK(hipMemsetAsync(qprev, 0, sizeof(double) * c->nloc, c->st));
+    double nq;
+    CHK(dot_host(c, q, q, &nq));
+    CHK(axpy_host(c, q, 1.0 / std::sqrt(nq) - 1.0, q));  // q /= ||q||
+    std::vector<double> al, be;
+    double beta = 0.0;
+    for (int it = 0; it < k; ++it) {
+        CHK(halo(c, q));
+        gk::StArgs a{};
+        a.x = q;
+        a.y = w;
+        CHK(stencil(c, gk::OP_PLAIN, gk::ACC_NONE, a));   // w = A q
+        if (beta != 0.0) CHK(axpy_host(c, w, -beta, qprev));
+        double alpha;
+        CHK(dot_host(c, w, q, &alpha));
+        CHK(axpy_host(c, w, -alpha, q));
+        double b2;
+        CHK(dot_host(c, w, w, &b2));
+        al.push_back(alpha);
+        beta = std::sqrt(b2);
+        if (beta == 0.0 || it == k - 1) break;
+        be.push_back(beta);
+        std::swap(qprev, q);                                // q_{j-1} <- q_j
+        HIPCHK(hipMemcpyAsync(q, w, sizeof(double) * c->nloc, hipMemcpyDeviceToDevice, c->st));
+        CHK(axpy_host(c, q, 1.0 / beta - 1.0, q));          // q_{j+1} = w / beta
+    }
+    be.resize(al.size() > 0 ? al.size() - 1 : 0);
+    *lmin = tridiag_eig(al, be, 0);
+    *lmax = tridiag_eig(al, be, (int)al.size() - 1);
+    HIPCHK(hipStreamSynchronize(c->st));
+    return GK_OK;
+}
+
+// ------------------------------------------- device vector primitives -------
+// Short-recurrence solvers (pcg_omp src/cg.f90:154-234, pbicgstab_omp
+// src/bicgstab.f90:91-182) on context-resident vectors: id 0 = x, 1 = b,
+// 2 .. m+2 = scratch (the Krylov columns).
+
+namespace {
+double *vec_of(gk_ctx *c, int id) {
+    if (id == GK_VEC_X) return c->x;
+    if (id == GK_VEC_B) return c->b;
+    if (id >= 2 && id <= c->m + 2) return c->V + (i64)(id - 2) * c->ld;
+    return nullptr;
+}
+}  // namespace
+
+extern "C" {
+
+int gk_vec_count(gk_ctx *c, int *count) {
+    CHK(check_ctx(c));
+    *count = c->m + 3;
+    return GK_OK;
+}
+
+int gk_vec_apply(gk_ctx *c, int what, int in, int out) {
+    CHK(check_ctx(c));
+    double *vi = vec_of(c, in), *vo = vec_of(c, out);
+    if (vi == nullptr || vo == nullptr || in == out || (what != 0 && what != 1))
+        return set_err(GK_ERR_ARG, "bad gk_vec_apply(%d, %d, %d)", what, in, out);
+    HIPCHK(hipSetDevice(c->dev));
+    c->cycle_mgs = c->cycle_hh = false;
+    if (what == 0) {
+        CHK(halo(c, vi));
+        gk::StArgs a{};
+        a.x = vi;
+        a.y = vo;
+        return stencil(c, gk::OP_PLAIN, gk::ACC_NONE, a);
+    }
+    if (c->pkind == GK_PREC_IDENTITY) {
+        HIPCHK(hipMemcpyAsync(vo, vi, sizeof(double) * c->nloc, hipMemcpyDeviceToDevice, c->st));
+        return GK_OK;
+    }
+    HIPCHK(hipMemcpyAsync(c->z, vi, sizeof(double) * c->nloc, hipMemcpyDeviceToDevice, c->st));
+    return precond_sweeps(c, vo, gk::ACC_NONE, nullptr, nullptr);
+}
+
+int gk_vec_dot(gk_ctx *c, int a, int b, double *result) {
+    CHK(check_ctx(c));
+    double *va = vec_of(c, a), *vb = vec_of(c, b);
+    if (va == nullptr || vb == nullptr || result == nullptr) return set_err(GK_ERR_ARG, "bad gk_vec_dot");
+    HIPCHK(hipSetDevice(c->dev));
+    return dot_host(c, va, vb, result);
+}
+
+int gk_vec_lincomb(gk_ctx *c, int form, int out, int a, int b, int cc, double s1, double s2) {
+    CHK(check_ctx(c));
+    double *vo = vec_of(c, out);
+    const double *va = vec_of(c, a), *vb = vec_of(c, b), *vc = vec_of(c, cc);
+    const bool need_a = form != GK_LC_ZERO, need_b = form == GK_LC_AXPY || form == GK_LC_AXPY2 ||
+                                                    form == GK_LC_XPAYMZ;
+    const bool need_c = form == GK_LC_AXPY2 || form == GK_LC_XPAYMZ;
+    if (vo == nullptr || form < 0 || form > GK_LC_ZERO || (need_a && va == nullptr) || (need_b && vb == nullptr) ||
+        (need_c && vc == nullptr))
+        return set_err(GK_ERR_ARG, "bad gk_vec_lincomb");
+    HIPCHK(hipSetDevice(c->dev));
+    gk::k_lincomb<<<c->nblk_stream, gk::TPB, 0, c->st>>>(form, vo, va, vb, vc, s1, s2, c->nloc);
+    LAUNCHCHK();
+    return GK_OK;
 }
 
 }  // extern "C"

@@ -257,6 +257,45 @@ __global__ __launch_bounds__(TPB) void k_add(double *__restrict__ x, const doubl
     for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) x[e] = x[e] + w[e];
 }
 
+// y = y + a x  (host scalar a)
+__global__ __launch_bounds__(TPB) void k_axpy_host(double *__restrict__ y, double a, const double *__restrict__ x,
+                                                   i64 n) {
+    const i64 stride = (i64)gridDim.x * TPB;
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) y[e] = y[e] + a * x[e];
+}
+
+// x[e] = deterministic pseudo-random value of the GLOBAL index g0+e in [-1,1)
+// (splitmix64), identical for any slab decomposition.
+__global__ __launch_bounds__(TPB) void k_fill_hash(double *__restrict__ x, i64 n, i64 g0, unsigned long long seed) {
+    const i64 stride = (i64)gridDim.x * TPB;
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) {
+        unsigned long long z = (unsigned long long)(g0 + e) + seed * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z = z ^ (z >> 31);
+        x[e] = (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+    }
+}
+
+// Linear combinations of the short-recurrence solvers, in the reference's
+// expression order (src/cg.f90:205-231, src/bicgstab.f90:131-180).
+enum { LC_COPY = 0, LC_AXPY = 1, LC_AXPY2 = 2, LC_XPAYMZ = 3, LC_ZERO = 4 };
+__global__ __launch_bounds__(TPB) void k_lincomb(int form, double *out, const double *a, const double *b,
+                                                 const double *c, double s1, double s2, i64 n) {
+    const i64 stride = (i64)gridDim.x * TPB;
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) {
+        double v;
+        switch (form) {
+            case LC_COPY: v = a[e]; break;
+            case LC_AXPY: v = a[e] + s1 * b[e]; break;                  // a + s1 b
+            case LC_AXPY2: v = a[e] + s1 * b[e] + s2 * c[e]; break;      // (a + s1 b) + s2 c
+            case LC_XPAYMZ: v = a[e] + s1 * (b[e] - s2 * c[e]); break;   // a + s1 (b - s2 c)
+            default: v = 0.0; break;
+        }
+        out[e] = v;
+    }
+}
+
 __global__ __launch_bounds__(TPB) void k_fill(double *__restrict__ x, double v, i64 n) {
     const i64 stride = (i64)gridDim.x * TPB;
     for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) x[e] = v;
@@ -313,7 +352,8 @@ __global__ __launch_bounds__(TPB) void k_hh_fix(double *__restrict__ w, i64 n, i
 //  step  (j >= 1): tmp = sqrt(tail); H(j+1,j) = w(j+1) > 0 ? -tmp : tmp
 //                  -> hcol[0..j-1] = w(1:j), hcol[j] = H(j+1,j), delta = -H (:306-316)
 __global__ void k_hh_pivot(const double *__restrict__ hb, const double *__restrict__ pin, int npin,
-                           int j, double *__restrict__ hcol, double *__restrict__ delta) {
+                           int j, double *__restrict__ hcol, double *__restrict__ delta,
+                           double *__restrict__ hcopy = nullptr) {
     __shared__ double sm[WAVES];
     const double s = sqrt(reduce_slab(pin, npin, sm));
     if (j == 0) {
@@ -325,10 +365,14 @@ __global__ void k_hh_pivot(const double *__restrict__ hb, const double *__restri
         }
         return;
     }
-    for (int k = threadIdx.x; k < j; k += blockDim.x) hcol[k] = hb[k];
+    for (int k = threadIdx.x; k < j; k += blockDim.x) {
+        hcol[k] = hb[k];
+        if (hcopy != nullptr) hcopy[k] = hb[k];
+    }
     if (threadIdx.x == 0) {
         const double H = (hb[j] > 0.0) ? -s : s;
         hcol[j] = H;
+        if (hcopy != nullptr) hcopy[j] = H;
         delta[0] = -H;
     }
 }

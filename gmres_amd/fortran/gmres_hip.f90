@@ -24,6 +24,8 @@ module gmres_hip_c
     implicit none
     integer(c_int), parameter :: GK_OK = 0
     integer(c_int), parameter :: GK_PREC_IDENTITY = 0, GK_PREC_CBPR2 = 1, GK_PREC_CHEB = 2
+    integer(c_int), parameter :: GK_VEC_X = 0, GK_VEC_B = 1
+    integer(c_int), parameter :: GK_LC_COPY = 0, GK_LC_AXPY = 1, GK_LC_AXPY2 = 2, GK_LC_XPAYMZ = 3, GK_LC_ZERO = 4
     interface
         function gk_last_error() result(p) bind(C, name='gk_last_error')
             import :: c_ptr
@@ -126,6 +128,17 @@ module gmres_hip_c
             integer(c_int), value :: j, precondition
             real(c_double), intent(out) :: hcol(*)
         end function
+        integer(c_int) function gk_hh_step_async(ctx, j, precondition) bind(C, name='gk_hh_step_async')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: j, precondition
+        end function
+        integer(c_int) function gk_hh_step_wait(ctx, j, hcol) bind(C, name='gk_hh_step_wait')
+            import :: c_int, c_ptr, c_double
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: j
+            real(c_double), intent(out) :: hcol(*)
+        end function
         integer(c_int) function gk_hh_update_x(ctx, y, n_out) bind(C, name='gk_hh_update_x')
             import :: c_int, c_ptr, c_double
             type(c_ptr), value :: ctx
@@ -137,6 +150,23 @@ module gmres_hip_c
             type(c_ptr), value :: ctx
             integer(c_int), value :: n_out
             real(c_double), intent(out) :: v_err(*)
+        end function
+        integer(c_int) function gk_vec_apply(ctx, what, vin, vout) bind(C, name='gk_vec_apply')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: what, vin, vout
+        end function
+        integer(c_int) function gk_vec_dot(ctx, a, b, res) bind(C, name='gk_vec_dot')
+            import :: c_int, c_ptr, c_double
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: a, b
+            real(c_double), intent(out) :: res
+        end function
+        integer(c_int) function gk_vec_lincomb(ctx, form, vout, a, b, c, s1, s2) bind(C, name='gk_vec_lincomb')
+            import :: c_int, c_ptr, c_double
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: form, vout, a, b, c
+            real(c_double), value :: s1, s2
         end function
         integer(c_size_t) function c_strlen(p) bind(C, name='strlen')
             import :: c_ptr, c_size_t
@@ -194,6 +224,33 @@ module gmres_hip_interfaces
     end interface
 end module gmres_hip_interfaces
 
+!> Table output in the reference's column layout (src/utils/utils.f90:37-51:
+!> print_header / print_line), so sweep tables diff 1:1 against the
+!> reference drivers' output (tests/strong_scaling.f90, tests/weak_scaling.f90).
+module gmres_hip_report
+    implicit none
+    private
+    public :: report_header, report_line
+contains
+    subroutine report_header(title)
+        character(len=*), intent(in) :: title
+        print *, title
+        write (*, '(A3, A10, A10, A10, A10, A14, A14, A14, A14, A14, A10, A15)') "#", "Vars", "Iters", &
+            "Restarts", "gmres(n)", "Tol.", "L2 Norm", "L_inf Norm", "Residual", "||I-V.t*V||", "Time", "Info"
+        write (*, '(150("-"))')
+    end subroutine report_header
+
+    subroutine report_line(test, nvars, seconds, iterations, restarts, m, tol, resid, verr, l2, linf, info)
+        integer, intent(in) :: test, nvars, iterations, restarts, m
+        real(8), intent(in) :: seconds, resid, verr, l2, linf, tol
+        character(len=*), intent(in) :: info
+        character(len=30) :: desc
+        desc = info
+        write (*, '(I3, I10, I10, I10, I10, ES14.2, ES14.4, ES14.4, ES14.4, ES14.4, F10.4, A20)') test, nvars, &
+            iterations, restarts, m, tol, l2, linf, resid, verr, seconds, desc
+    end subroutine report_line
+end module gmres_hip_report
+
 module gmres_hip
     use, intrinsic :: iso_c_binding
     use gmres_hip_c
@@ -211,6 +268,7 @@ module gmres_hip
     public :: stencil_vector, precond
     public :: hip_poisson5, hip_identity, hip_cbpr2, hip_chebyshev
     public :: gmres_mgsr_hip, gmres_hh_hip, gmres_hh_prec_hip, hip_release
+    public :: pcg_hip, pbicgstab_hip, pcg_drive, bicgstab_drive
     public :: mgsr_drive, hh_drive, givens_column, back_solve
 
     type(c_ptr) :: opctx = c_null_ptr   ! context of the host-array plug-ins
@@ -369,10 +427,16 @@ contains
             g = 0.0d0; H = 0.0d0
             st = gk_hh_cycle_start(ctx, precondition, g1); if (st /= GK_OK) return
             g(1) = g1
+            if (.not. converged) then
+                st = gk_hh_step_async(ctx, 1, precondition); if (st /= GK_OK) return
+            end if
             do j = 1, m
                 if (converged) exit
                 n_out = j
-                st = gk_hh_step(ctx, j, precondition, hcol); if (st /= GK_OK) return
+                if (j < m) then  ! pipelined as in mgsr_drive
+                    st = gk_hh_step_async(ctx, j + 1, precondition); if (st /= GK_OK) return
+                end if
+                st = gk_hh_step_wait(ctx, j, hcol); if (st /= GK_OK) return
                 H(1:j + 1, j) = hcol(1:j + 1)
                 call givens_column(H, cs, sn, g, j)
                 final_err(j) = abs(g(j + 1))/beta0
@@ -397,6 +461,144 @@ contains
         end if
         st = gk_get_x(ctx, x)
     end function hh_drive
+
+    !> Preconditioned CG, gmres-free sibling on the same seam: pcg_omp
+    !> (src/cg.f90:154-234) with its scalars on the host and every vector on
+    !> the device.  iter: in = max iterations, out = first i with res < tol.
+    integer function pcg_drive(ctx, tol, iter, res, want_hist, hist) result(st)
+        type(c_ptr), intent(in) :: ctx
+        real(8), intent(in) :: tol
+        integer, intent(inout) :: iter
+        real(8), intent(out) :: res
+        logical, intent(in) :: want_hist
+        real(8), intent(inout) :: hist(*)
+        integer(c_int), parameter :: VR = 2, VZ = 3, VP = 4, VAX = 5
+        real(8) :: rr, pap, alpha, beta, rsq
+        integer :: i, maxit
+        logical :: converged
+        converged = .false.
+        maxit = iter
+        res = 0.0d0
+        st = gk_vec_lincomb(ctx, GK_LC_ZERO, GK_VEC_X, GK_VEC_X, GK_VEC_X, GK_VEC_X, 0.0d0, 0.0d0)
+        if (st /= GK_OK) return
+        st = gk_vec_lincomb(ctx, GK_LC_COPY, VR, GK_VEC_B, GK_VEC_B, GK_VEC_B, 0.0d0, 0.0d0); if (st /= GK_OK) return
+        st = gk_vec_apply(ctx, 1_c_int, VR, VZ); if (st /= GK_OK) return              ! z = M^-1 r
+        st = gk_vec_lincomb(ctx, GK_LC_COPY, VP, VZ, VZ, VZ, 0.0d0, 0.0d0); if (st /= GK_OK) return
+        do i = 1, maxit
+            if (converged) exit
+            st = gk_vec_apply(ctx, 0_c_int, VP, VAX); if (st /= GK_OK) return       ! ax = A p
+            st = gk_vec_dot(ctx, VR, VZ, rr); if (st /= GK_OK) return
+            st = gk_vec_dot(ctx, VAX, VP, pap); if (st /= GK_OK) return
+            alpha = rr/pap
+            st = gk_vec_lincomb(ctx, GK_LC_AXPY, GK_VEC_X, GK_VEC_X, VP, VP, alpha, 0.0d0); if (st /= GK_OK) return
+            st = gk_vec_lincomb(ctx, GK_LC_AXPY, VR, VR, VAX, VAX, -alpha, 0.0d0); if (st /= GK_OK) return
+            st = gk_vec_dot(ctx, VR, VR, rsq); if (st /= GK_OK) return
+            st = gk_vec_apply(ctx, 1_c_int, VR, VZ); if (st /= GK_OK) return        ! z = M^-1 r
+            st = gk_vec_dot(ctx, VR, VZ, beta); if (st /= GK_OK) return
+            res = sqrt(rsq)
+            beta = beta/rr
+            if (want_hist) hist(i) = res
+            if (res < tol) then
+                converged = .true.
+                iter = i
+            end if
+            st = gk_vec_lincomb(ctx, GK_LC_AXPY, VP, VZ, VP, VP, beta, 0.0d0); if (st /= GK_OK) return  ! p = z + beta p
+        end do
+    end function pcg_drive
+
+    !> Preconditioned BiCGSTAB: pbicgstab_omp (src/bicgstab.f90:91-182); the
+    !> reference's uninitialised first-iteration accumulators are taken as 0.
+    integer function bicgstab_drive(ctx, tol, max_iter, res, want_hist, hist) result(st)
+        type(c_ptr), intent(in) :: ctx
+        real(8), intent(in) :: tol
+        integer, intent(inout) :: max_iter
+        real(8), intent(out) :: res
+        logical, intent(in) :: want_hist
+        real(8), intent(inout) :: hist(*)
+        integer(c_int), parameter :: VR = 2, VR0 = 3, VAP = 4, VS = 5, VAS = 6, VP = 7, VZ1 = 8, VZ2 = 9
+        real(8) :: rr0, ap_r0, as_s, as_as, r_r0_new, alpha, omega, beta, rsq
+        integer :: i, iters
+        logical :: converged
+        converged = .false.
+        iters = max_iter
+        res = 0.0d0
+        st = gk_vec_lincomb(ctx, GK_LC_ZERO, GK_VEC_X, GK_VEC_X, GK_VEC_X, GK_VEC_X, 0.0d0, 0.0d0)
+        if (st /= GK_OK) return
+        st = gk_vec_lincomb(ctx, GK_LC_COPY, VR, GK_VEC_B, GK_VEC_B, GK_VEC_B, 0.0d0, 0.0d0); if (st /= GK_OK) return
+        st = gk_vec_lincomb(ctx, GK_LC_COPY, VR0, VR, VR, VR, 0.0d0, 0.0d0); if (st /= GK_OK) return
+        st = gk_vec_lincomb(ctx, GK_LC_COPY, VP, VR0, VR0, VR0, 0.0d0, 0.0d0); if (st /= GK_OK) return
+        do i = 1, max_iter
+            if (converged) exit
+            st = gk_vec_apply(ctx, 1_c_int, VP, VZ1); if (st /= GK_OK) return      ! z1 = M^-1 p
+            st = gk_vec_apply(ctx, 0_c_int, VZ1, VAP); if (st /= GK_OK) return     ! ap = A z1
+            st = gk_vec_dot(ctx, VR, VR0, rr0); if (st /= GK_OK) return
+            st = gk_vec_dot(ctx, VAP, VR0, ap_r0); if (st /= GK_OK) return
+            alpha = rr0/ap_r0
+            st = gk_vec_lincomb(ctx, GK_LC_AXPY, VS, VR, VAP, VAP, -alpha, 0.0d0); if (st /= GK_OK) return
+            st = gk_vec_apply(ctx, 1_c_int, VS, VZ2); if (st /= GK_OK) return      ! z2 = M^-1 s
+            st = gk_vec_apply(ctx, 0_c_int, VZ2, VAS); if (st /= GK_OK) return     ! as = A z2
+            st = gk_vec_dot(ctx, VAS, VS, as_s); if (st /= GK_OK) return
+            st = gk_vec_dot(ctx, VAS, VAS, as_as); if (st /= GK_OK) return
+            omega = as_s/as_as
+            st = gk_vec_lincomb(ctx, GK_LC_AXPY2, GK_VEC_X, GK_VEC_X, VZ1, VZ2, alpha, omega); if (st /= GK_OK) return
+            st = gk_vec_lincomb(ctx, GK_LC_AXPY, VR, VS, VAS, VAS, -omega, 0.0d0); if (st /= GK_OK) return
+            st = gk_vec_dot(ctx, VR, VR, rsq); if (st /= GK_OK) return
+            res = sqrt(rsq)
+            if (want_hist) hist(i) = res
+            if (res < tol) then
+                iters = i
+                converged = .true.
+            end if
+            st = gk_vec_dot(ctx, VR, VR0, r_r0_new); if (st /= GK_OK) return
+            beta = (r_r0_new/rr0)*(alpha/omega)
+            st = gk_vec_lincomb(ctx, GK_LC_XPAYMZ, VP, VR, VP, VAP, beta, omega); if (st /= GK_OK) return
+        end do
+        max_iter = iters
+    end function bicgstab_drive
+
+    !> Drop-in for pcg_omp (src/cg.f90:154-162).
+    subroutine pcg_hip(Ax_op, b, x, tol, iter, res, M_inv, params)
+        procedure(stencil_vector) :: Ax_op
+        real(8), intent(in) :: b(:)
+        real(8), allocatable, intent(out) :: x(:)
+        real(8), intent(in) :: tol
+        integer, intent(inout) :: iter
+        real(8), intent(out) :: res
+        procedure(precond) :: M_inv
+        real(8), intent(in) :: params(:)
+        type(c_ptr) :: ctx
+        integer(c_int) :: kind, degree
+        real(8) :: dummy(1)
+        call require_device_op(Ax_op, 'pcg_hip')
+        call prec_kind(M_inv, params, kind, degree)
+        allocate (x(size(b)))
+        ctx = solver_ctx(b, 8, kind, degree, params)
+        call gk_require(pcg_drive(ctx, tol, iter, res, .false., dummy), 'pcg_hip')
+        call gk_require(gk_get_x(ctx, x), 'gk_get_x')
+        call gk_require(gk_destroy(ctx), 'gk_destroy')
+    end subroutine pcg_hip
+
+    !> Drop-in for pbicgstab_omp (src/bicgstab.f90:91-99).
+    subroutine pbicgstab_hip(ax_op, b, x, tol, max_iter, res, m_inv, params)
+        procedure(stencil_vector) :: ax_op
+        real(8), intent(in) :: b(:)
+        real(8), allocatable, intent(out) :: x(:)
+        real(8), intent(in) :: tol
+        integer, intent(inout) :: max_iter
+        real(8), intent(out) :: res
+        procedure(precond) :: m_inv
+        real(8), intent(in) :: params(:)
+        type(c_ptr) :: ctx
+        integer(c_int) :: kind, degree
+        real(8) :: dummy(1)
+        call require_device_op(ax_op, 'pbicgstab_hip')
+        call prec_kind(m_inv, params, kind, degree)
+        allocate (x(size(b)))
+        ctx = solver_ctx(b, 8, kind, degree, params)
+        call gk_require(bicgstab_drive(ctx, tol, max_iter, res, .false., dummy), 'pbicgstab_hip')
+        call gk_require(gk_get_x(ctx, x), 'gk_get_x')
+        call gk_require(gk_destroy(ctx), 'gk_destroy')
+    end subroutine pbicgstab_hip
 
     ! ------------------------------------------------ host-array plug-ins --
 
@@ -654,3 +856,35 @@ integer(c_int) function gmres_hh_hip_run(ctx, m, tol, precondition, midcycle_exi
                                 hist_ferr, nc)
     n_out = no; stages_out = so; n_cycles = nc
 end function gmres_hh_hip_run
+
+integer(c_int) function pcg_hip_run(ctx, tol, iter, res, want_hist, hist) bind(C, name='pcg_hip_run')
+    use, intrinsic :: iso_c_binding
+    use gmres_hip, only: pcg_drive
+    implicit none
+    type(c_ptr), value :: ctx
+    real(c_double), value :: tol
+    integer(c_int), intent(inout) :: iter
+    real(c_double), intent(out) :: res
+    integer(c_int), value :: want_hist
+    real(c_double), intent(inout) :: hist(*)
+    integer :: it
+    it = iter
+    pcg_hip_run = pcg_drive(ctx, tol, it, res, want_hist /= 0, hist)
+    iter = it
+end function pcg_hip_run
+
+integer(c_int) function pbicgstab_hip_run(ctx, tol, max_iter, res, want_hist, hist) bind(C, name='pbicgstab_hip_run')
+    use, intrinsic :: iso_c_binding
+    use gmres_hip, only: bicgstab_drive
+    implicit none
+    type(c_ptr), value :: ctx
+    real(c_double), value :: tol
+    integer(c_int), intent(inout) :: max_iter
+    real(c_double), intent(out) :: res
+    integer(c_int), value :: want_hist
+    real(c_double), intent(inout) :: hist(*)
+    integer :: it
+    it = max_iter
+    pbicgstab_hip_run = bicgstab_drive(ctx, tol, it, res, want_hist /= 0, hist)
+    max_iter = it
+end function pbicgstab_hip_run

@@ -180,6 +180,14 @@ class Context:
         nat.check(nat.hip().gk_true_residual(self._h, ctypes.byref(v)), "gk_true_residual")
         return v.value
 
+    def lanczos_bounds(self, k: int = 40) -> tuple[float, float]:
+        """Extreme Ritz values of A after k Lanczos steps (spectrum estimate
+        for the Chebyshev preconditioner interval)."""
+        lo, hi = ctypes.c_double(), ctypes.c_double()
+        nat.check(nat.hip().gk_lanczos_bounds(self._h, int(k), ctypes.byref(lo), ctypes.byref(hi)),
+                  "gk_lanczos_bounds")
+        return lo.value, hi.value
+
     # -- Arnoldi pieces (for tests / custom drivers) -----------------------
     def mgs_cycle_start(self) -> float:
         v = ctypes.c_double()
@@ -268,6 +276,28 @@ def gmres_hh(ctx: Context, tol: float = 1e-15, precondition: bool = False, midcy
         r.hist_res = hr[: nc.value].copy()
         r.hist_ferr = hf.reshape(max_cycles, m)[: nc.value].copy()
     return r
+
+
+def _short(fn_name: str, ctx: Context, tol: float, max_iter: int, want_hist: bool):
+    if ctx.m < 8:
+        raise ValueError("short-recurrence solvers need a context with m >= 8 (scratch vectors)")
+    it = ctypes.c_int(max_iter)
+    res = ctypes.c_double()
+    hist = np.zeros(max_iter if want_hist else 1)
+    nat.check(getattr(nat.fhost(), fn_name)(ctx.handle, tol, ctypes.byref(it), ctypes.byref(res), int(want_hist),
+                                            _p(hist)), fn_name)
+    x = ctx.get_x()
+    return x, it.value, res.value, (hist[: np.count_nonzero(hist)].copy() if want_hist else None)
+
+
+def pcg(ctx: Context, tol: float = 1e-9, max_iter: int = 1000, want_hist: bool = False):
+    """pcg_omp (src/cg.f90:154-234) on the device: (x, iter, res, hist)."""
+    return _short("pcg_hip_run", ctx, tol, max_iter, want_hist)
+
+
+def pbicgstab(ctx: Context, tol: float = 1e-9, max_iter: int = 1000, want_hist: bool = False):
+    """pbicgstab_omp (src/bicgstab.f90:91-182) on the device: (x, iters, res, hist)."""
+    return _short("pbicgstab_hip_run", ctx, tol, max_iter, want_hist)
 
 
 # ---------------------------------------------------------------- kernels ---

@@ -129,11 +129,42 @@ int gk_hh_cycle_start(gk_ctx *ctx, int precondition, double *g1);
  * hcol[0..j] = H(1:j+1,j) (H(j+1,j) = -sign(||w(j+1:n)||, w(j+1)));
  * builds P(:,j+1)  (:255-321 / :438-502). */
 int gk_hh_step(gk_ctx *ctx, int j, int precondition, double *hcol);
+/* Split form of gk_hh_step (see gk_mgs_step_async). */
+int gk_hh_step_async(gk_ctx *ctx, int j, int precondition);
+int gk_hh_step_wait(gk_ctx *ctx, int j, double *hcol);
 /* x += P_1..P_n_out [y;0]  (:350-378). */
 int gk_hh_update_x(gk_ctx *ctx, const double *y, int n_out);
 /* calculate_verr (:568-593): v_err(i) = sum_{j<i} 2 (V_i.V_j)^2, V rebuilt
  * from the reflectors on device (extra n x n_out buffer). */
 int gk_hh_verr(gk_ctx *ctx, int n_out, double *v_err);
+
+/* ------------------------------------------------ spectrum estimate ---- */
+/* k Lanczos steps on A from a deterministic pseudo-random start vector (the
+ * same for any slab decomposition); returns the extreme Ritz values of the
+ * k x k tridiagonal (Sturm bisection on the host).  The README-promised
+ * eigenvalue estimate for the Chebyshev parameters (README.md:11; the
+ * reference hard-codes params, chebyshev.f90:20).  Clobbers work vectors. */
+int gk_lanczos_bounds(gk_ctx *ctx, int k, double *lmin, double *lmax);
+
+/* ------------------------------------------- device vector primitives ---- */
+/* For the short-recurrence solvers that share the operator / preconditioner
+ * seam (pcg_omp src/cg.f90:154-234, pbicgstab_omp src/bicgstab.f90:91-182):
+ * context-resident vectors by id: GK_VEC_X = x, GK_VEC_B = b, 2 .. m+2 =
+ * scratch (the Krylov columns).  Scalars come back to the host, as the
+ * reference computes them in `single` blocks. */
+#define GK_VEC_X 0
+#define GK_VEC_B 1
+#define GK_LC_COPY 0   /* out = a                  */
+#define GK_LC_AXPY 1   /* out = a + s1*b           */
+#define GK_LC_AXPY2 2  /* out = (a + s1*b) + s2*c  */
+#define GK_LC_XPAYMZ 3 /* out = a + s1*(b - s2*c)  */
+#define GK_LC_ZERO 4   /* out = 0                  */
+int gk_vec_count(gk_ctx *ctx, int *count);
+/* what = 0: out = A in; what = 1: out = M^-1 in (in != out). */
+int gk_vec_apply(gk_ctx *ctx, int what, int in, int out);
+/* result = <a, b> over all ranks (synchronous). */
+int gk_vec_dot(gk_ctx *ctx, int a, int b, double *result);
+int gk_vec_lincomb(gk_ctx *ctx, int form, int out, int a, int b, int c, double s1, double s2);
 
 /* ---------------------------------------------------------- profiling ---- */
 /* enable = 1: every launch is bracketed by HIP events on the context stream;

@@ -15,6 +15,8 @@
  *   - gmres_hh_omp     src/gmres_hh.f90:211-385    (midcycle_exit = 0)
  *   - gmres_hh_prec_omp src/gmres_hh.f90:388-566   (midcycle_exit = 1)
  *   - calculate_verr   src/gmres_hh.f90:568-593
+ *   - pcg_omp          src/cg.f90:154-234
+ *   - pbicgstab_omp    src/bicgstab.f90:91-182
  * plus two things the reference does not have:
  *   - an identity preconditioner (config 1 "no precond");
  *   - Chebyshev(k), the build-defined degree-k polynomial preconditioner of
@@ -531,4 +533,115 @@ int or_gmres_hh(const double *b, int N, int m, double tol, int prec, const doubl
     free(P); free(H); free(w); free(z); free(vj); free(aux); free(aux2);
     free(g); free(y); free(cs); free(sn);
     return cut;
+}
+
+/* -------------------------------------------------------- CG / BiCGSTAB ---- */
+
+/* pcg_omp (src/cg.f90:154-234): x0 = 0, r = b, z = M^-1 r, p = z; per
+ * iteration rr = <r,z>, alpha = rr/<Ap,p>; x += alpha p; r -= alpha Ap;
+ * res = sqrt(<r,r>); z = M^-1 r; beta = <r,z>/rr; p = z + beta p.
+ * *iter in: max iterations, out: first i with res < tol (unchanged if never).
+ * hist_res[i-1] = res of iteration i (may be NULL). */
+void or_pcg(const double *b, int N, double tol, int *iter, double *res_out, int prec, const double *params,
+            int degree, double *x, double *hist_res) {
+    const i64 n = (i64)N * N;
+    double *ax = (double *)malloc(sizeof(double) * n), *p = (double *)malloc(sizeof(double) * n);
+    double *r = (double *)malloc(sizeof(double) * n), *z = (double *)malloc(sizeof(double) * n);
+    double *aux = (double *)malloc(sizeof(double) * n), *aux2 = (double *)malloc(sizeof(double) * n);
+    int maxit = *iter, converged = 0;
+    double res = 0.0;
+    for (i64 j = 0; j < n; ++j) {
+        x[j] = 0.0;
+        r[j] = b[j];
+    }
+    or_precond(prec, r, z, aux, aux2, params, degree, N);
+    for (i64 j = 0; j < n; ++j) p[j] = z[j];
+    for (int i = 1; i <= maxit; ++i) {
+        if (converged) break;
+        or_stvec(p, ax, N);
+        double rr = 0.0, alpha = 0.0, beta = 0.0;
+        res = 0.0;
+        for (i64 j = 0; j < n; ++j) {
+            rr = rr + r[j] * z[j];
+            alpha = alpha + ax[j] * p[j];
+        }
+        alpha = rr / alpha;
+        for (i64 j = 0; j < n; ++j) {
+            x[j] = x[j] + alpha * p[j];
+            r[j] = r[j] - alpha * ax[j];
+            res = res + r[j] * r[j];
+        }
+        or_precond(prec, r, z, aux, aux2, params, degree, N);
+        for (i64 j = 0; j < n; ++j) beta = beta + r[j] * z[j];
+        res = sqrt(res);
+        beta = beta / rr;
+        if (hist_res) hist_res[i - 1] = res;
+        if (res < tol) {
+            converged = 1;
+            *iter = i;
+        }
+        for (i64 j = 0; j < n; ++j) p[j] = z[j] + beta * p[j];
+    }
+    *res_out = res;
+    free(ax); free(p); free(r); free(z); free(aux); free(aux2);
+}
+
+/* pbicgstab_omp (src/bicgstab.f90:91-182); the reference leaves its dot
+ * accumulators uninitialised before the first iteration (:102, :123-126):
+ * they start at 0 here. */
+void or_pbicgstab(const double *b, int N, double tol, int *max_iter, double *res_out, int prec,
+                  const double *params, int degree, double *x, double *hist_res) {
+    const i64 n = (i64)N * N;
+    double *r = (double *)malloc(sizeof(double) * n), *r0 = (double *)malloc(sizeof(double) * n);
+    double *ap = (double *)malloc(sizeof(double) * n), *s = (double *)malloc(sizeof(double) * n);
+    double *as = (double *)malloc(sizeof(double) * n), *p = (double *)malloc(sizeof(double) * n);
+    double *z1 = (double *)malloc(sizeof(double) * n), *z2 = (double *)malloc(sizeof(double) * n);
+    double *aux = (double *)malloc(sizeof(double) * n), *aux2 = (double *)malloc(sizeof(double) * n);
+    int converged = 0, iters = *max_iter;
+    double rr0 = 0.0, ap_r0 = 0.0, as_s = 0.0, as_as = 0.0, r_r0_new = 0.0, res = 0.0;
+    for (i64 j = 0; j < n; ++j) {
+        x[j] = 0.0;
+        r[j] = b[j];
+        r0[j] = r[j];
+        p[j] = r0[j];
+    }
+    for (int i = 1; i <= *max_iter; ++i) {
+        if (converged) break;
+        or_precond(prec, p, z1, aux, aux2, params, degree, N);
+        or_stvec(z1, ap, N);
+        for (i64 j = 0; j < n; ++j) {
+            rr0 = rr0 + r[j] * r0[j];
+            ap_r0 = ap_r0 + ap[j] * r0[j];
+        }
+        double alpha = rr0 / ap_r0;
+        for (i64 j = 0; j < n; ++j) s[j] = r[j] - alpha * ap[j];
+        or_precond(prec, s, z2, aux, aux2, params, degree, N);
+        or_stvec(z2, as, N);
+        for (i64 j = 0; j < n; ++j) {
+            as_s = as_s + as[j] * s[j];
+            as_as = as_as + as[j] * as[j];
+        }
+        double omega = as_s / as_as;
+        for (i64 j = 0; j < n; ++j) {
+            x[j] = x[j] + alpha * z1[j] + omega * z2[j];
+            r[j] = s[j] - omega * as[j];
+        }
+        res = or_norm2(r, n);
+        if (hist_res) hist_res[i - 1] = res;
+        if (res < tol) {
+            iters = i;
+            converged = 1;
+        }
+        for (i64 j = 0; j < n; ++j) r_r0_new = r_r0_new + r[j] * r0[j];
+        double beta = (r_r0_new / rr0) * (alpha / omega);
+        r_r0_new = 0.0;
+        as_s = 0.0;
+        as_as = 0.0;
+        rr0 = 0.0;
+        ap_r0 = 0.0;
+        for (i64 j = 0; j < n; ++j) p[j] = r[j] + beta * (p[j] - omega * ap[j]);
+    }
+    *max_iter = iters;
+    *res_out = res;
+    free(r); free(r0); free(ap); free(s); free(as); free(p); free(z1); free(z2); free(aux); free(aux2);
 }

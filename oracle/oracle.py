@@ -58,6 +58,9 @@ def lib():
         L.or_gmres_mgsr.restype = ctypes.c_int
         L.or_gmres_hh.argtypes = common
         L.or_gmres_hh.restype = ctypes.c_int
+        kry = [_dp, ctypes.c_int, ctypes.c_double, _ip, _dp, ctypes.c_int, _dp, ctypes.c_int, _dp, _dp]
+        L.or_pcg.argtypes = kry
+        L.or_pbicgstab.argtypes = kry
         _lib = L
     return _lib
 
@@ -170,3 +173,25 @@ def gmres_hh(b, N, m, tol=1e-15, prec=PREC_IDENTITY, params=(8.2, 0.2), degree=8
     """gmres_hh_omp (midcycle_exit=0, prec must be identity) / gmres_hh_prec_omp (=1)."""
     return _solve(lib().or_gmres_hh, b, N, m, tol, prec, params, degree, midcycle_exit,
                   max_cycles, step_limit, threads)
+
+
+def _short_recurrence(fn, b, N, tol, max_iter, prec, params, degree):
+    b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1)
+    x = np.zeros(N * N)
+    it = ctypes.c_int(max_iter)
+    res = ctypes.c_double()
+    hist = np.zeros(max_iter)
+    pr = np.asarray(params, dtype=np.float64)
+    fn(_p(b), N, tol, ctypes.byref(it), ctypes.byref(res), prec, _p(pr), degree, _p(x), _p(hist))
+    k = int(np.count_nonzero(hist))
+    return x, it.value, res.value, hist[:k].copy()
+
+
+def pcg(b, N, tol=1e-9, max_iter=1000, prec=PREC_IDENTITY, params=(8.2, 0.2), degree=8):
+    """pcg_omp (src/cg.f90:154-234): returns (x, iter, res, per-iteration res)."""
+    return _short_recurrence(lib().or_pcg, b, N, tol, max_iter, prec, params, degree)
+
+
+def pbicgstab(b, N, tol=1e-9, max_iter=1000, prec=PREC_IDENTITY, params=(8.2, 0.2), degree=8):
+    """pbicgstab_omp (src/bicgstab.f90:91-182): returns (x, iters, res, per-iteration res)."""
+    return _short_recurrence(lib().or_pbicgstab, b, N, tol, max_iter, prec, params, degree)

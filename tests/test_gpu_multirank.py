@@ -93,3 +93,51 @@ def test_slabs_converge_and_verr():
     assert 0 <= res[0].v_err[res[0].n_out - 1] < 1e-12
     ref = _single(N, m, "mgsr", "cbpr2", 1, 1000)
     assert abs(res[0].iterations - ref.iterations) <= max(2, 0.01 * ref.iterations)
+
+
+def test_lanczos_independent_of_decomposition():
+    import gmres_amd as ga
+
+    N = 40
+    with ga.Context(N, 8) as c:
+        ref = c.lanczos_bounds(30)
+    parts = ga.slab_partition(N, 3)
+    g = ga.LocalGroup(3)
+    ctxs = [ga.Context(N, 8, line0=l0, nlines=nl) for l0, nl in parts]
+    for r, c in enumerate(ctxs):
+        c.comm_init_local(g, r, max(nl for _, nl in parts))
+    out = [None] * 3
+
+    def work(r):
+        out[r] = ctxs[r].lanczos_bounds(30)
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert out[0] == out[1] == out[2]
+    assert out[0][0] == pytest.approx(ref[0], rel=1e-9) and out[0][1] == pytest.approx(ref[1], rel=1e-12)
+    for c in ctxs:
+        c.close()
+    g.close()
+
+
+@pytest.mark.parametrize("method,prec", [("mgsr", "cbpr2"), ("hh", "identity")])
+def test_rccl_one_rank_communicator(monkeypatch, method, prec):
+    """The RCCL code path on one GPU: a 1-rank communicator (GK_FORCE_RCCL=1)
+    routes every slab all-reduce, broadcast and (empty) halo group through
+    RCCL on the context stream; results must equal the communicator-free run
+    bit for bit (a 1-rank sum is exact)."""
+    import gmres_amd as ga
+
+    N, m = 64, 16
+    ref = _single(N, m, method, prec, 1, 4)
+    monkeypatch.setenv("GK_FORCE_RCCL", "1")
+    with ga.Context(N, m) as c:
+        c.comm_init(1, 0, N, ga.Context.unique_id())
+        c.set_precond(prec, (8.2, 0.2), 1)
+        c.set_rhs_ones()
+        r = _solve(c, method, prec, 4)
+    assert np.array_equal(r.hist_res, ref.hist_res)
+    assert np.array_equal(r.x, ref.x)

@@ -127,3 +127,16 @@ def test_step_limit_sample(oracle):
     b = oracle.rhs_ones(64)
     r = oracle.gmres_mgsr(b, 64, 30, variant=oracle.MGSR_OMP, step_limit=7)
     assert r.cut and np.all(np.diff(r.step_times) >= 0) and r.step_times[6] > 0
+
+
+@pytest.mark.parametrize("solver", ["pcg", "pbicgstab"])
+def test_short_recurrence_oracle_converges(oracle, solver):
+    N = 48
+    for kind in (oracle.PREC_IDENTITY, oracle.PREC_CBPR2):
+        x, it, res, hist = getattr(oracle, solver)(oracle.rhs_ones(N), N, 1e-9, 5000, kind)
+        assert res < 1e-9 and it == len(hist)
+        assert np.max(np.abs(x - 1.0)) < 1e-6
+    # the preconditioner cuts the iteration count
+    _, it_id, _, _ = getattr(oracle, solver)(oracle.rhs_ones(N), N, 1e-9, 5000, oracle.PREC_IDENTITY)
+    _, it_pc, _, _ = getattr(oracle, solver)(oracle.rhs_ones(N), N, 1e-9, 5000, oracle.PREC_CBPR2)
+    assert it_pc < it_id
