@@ -117,6 +117,8 @@ struct gk_ctx {
     int vec = 2, JT = 16;
     dim3 sgrid;
     int np_st = 0, np_pj = 0, nblk_stream = 0;
+    int last_np = 0;          // partial count written by the last ACC-carrying sweep
+    int tune_cheb_fused = 1;  // temporal-blocked Chebyshev sweeps (single slab)
     // tuning knobs (gk_set_tuning)
     int tune_nt = -1, tune_pj_blocks = 0, tune_st_blocks = 0;  // tune_nt: -1 auto
     bool nt_auto = false;
@@ -354,6 +356,7 @@ int launch_stencil_a(gk_ctx *c, int acc, const gk::StArgs &a) {
 
 int stencil(gk_ctx *c, int op, int acc, gk::StArgs a) {
     ProfScope ps(c, GK_KID_STENCIL);
+    if (acc != gk::ACC_NONE) c->last_np = c->np_st;
     a.hlo = halo_lo(c);
     a.hhi = halo_hi(c);
     a.N = c->N;
@@ -474,6 +477,85 @@ int op_precond(gk_ctx *c, const double *v, double *out, bool resid, int acc, con
     return precond_sweeps(c, out, acc, vdot, part);
 }
 
+template <int L, bool FIRST, bool LAST>
+int launch_cf_acc(gk_ctx *c, dim3 g, int acc, const gk::CFArgs &a) {
+    if (acc == gk::ACC_DOT) gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_DOT><<<g, gk::CF_W, 0, c->st>>>(a);
+    else if (acc == gk::ACC_NORM) gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NORM><<<g, gk::CF_W, 0, c->st>>>(a);
+    else gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NONE><<<g, gk::CF_W, 0, c->st>>>(a);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
+template <bool FIRST, bool LAST>
+int launch_cf(gk_ctx *c, int L, dim3 g, int acc, const gk::CFArgs &a) {
+    switch (L) {
+        case 1: return launch_cf_acc<1, FIRST, LAST>(c, g, acc, a);
+        case 2: return launch_cf_acc<2, FIRST, LAST>(c, g, acc, a);
+        case 3: return launch_cf_acc<3, FIRST, LAST>(c, g, acc, a);
+        default: return launch_cf_acc<4, FIRST, LAST>(c, g, acc, a);
+    }
+}
+
+// Chebyshev(k <= 8) as one or two temporal-blocked passes (k_cheb_fused):
+// sweeps 1..min(k,4) in the first, the rest in the second.
+int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part, const double *c1,
+               const double *c2, double theta) {
+    ProfScope ps(c, GK_KID_STENCIL);
+    const int k = c->pdeg;
+    const int g1 = std::min(k, gk::CF_LMAX), g2 = k - g1;
+    auto grid = [&](int L, int &JT) {
+        const int H = L + (L & 1);
+        const int gx = (c->N + (gk::CF_PTS - 2 * H) - 1) / (gk::CF_PTS - 2 * H);
+        JT = 64;
+        int gy = (c->nlines + JT - 1) / JT;
+        while ((i64)gx * gy > gk::NPMAX) {
+            JT *= 2;
+            gy = (c->nlines + JT - 1) / JT;
+        }
+        return dim3(gx, gy, 1);
+    };
+    gk::CFArgs a{};
+    a.N = c->N;
+    a.nlines = c->nlines;
+    a.theta = theta;
+    a.din = c->z;
+    a.vdot = vdot;
+    a.part = part;
+    for (int l = 0; l < g1; ++l) {
+        a.c1[l] = c1[l];
+        a.c2[l] = c2[l];
+    }
+    int JT;
+    dim3 g = grid(g1, JT);
+    a.JT = JT;
+    if (g2 == 0) {
+        a.out = out;
+        if (acc != gk::ACC_NONE) c->last_np = g.x * g.y;
+        return launch_cf<true, true>(c, g1, g, acc, a);
+    }
+    a.dout = c->dA;
+    a.rout = c->aux;
+    a.zout = c->dB;
+    CHK((launch_cf<true, false>(c, g1, g, gk::ACC_NONE, a)));
+    gk::CFArgs b{};
+    b.N = c->N;
+    b.nlines = c->nlines;
+    b.din = c->dA;
+    b.rin = c->aux;
+    b.zin = c->dB;
+    b.out = out;
+    b.vdot = vdot;
+    b.part = part;
+    for (int l = 0; l < g2; ++l) {
+        b.c1[l] = c1[g1 + l];
+        b.c2[l] = c2[g1 + l];
+    }
+    g = grid(g2, JT);
+    b.JT = JT;
+    if (acc != gk::ACC_NONE) c->last_np = g.x * g.y;
+    return launch_cf<false, true>(c, g2, g, acc, b);
+}
+
 // out = M^-1 z for z already in c->z (cbpr2 or Chebyshev sweeps).
 int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *part) {
     CHK(halo(c, c->z));
@@ -501,6 +583,16 @@ int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *
     const double delta = std::fabs(c->p1 - c->p0) / 2.0;
     const double sigma = theta / delta;
     double rho0 = delta / theta;
+    if (c->tune_cheb_fused && !collective(c) && c->N % 2 == 0 && c->pdeg <= 2 * gk::CF_LMAX) {
+        double c1[2 * gk::CF_LMAX], c2[2 * gk::CF_LMAX];
+        for (int it = 0; it < c->pdeg; ++it) {
+            const double rho1 = 1.0 / (2.0 * sigma - rho0);
+            c1[it] = rho1 * rho0;
+            c2[it] = 2.0 * rho1 / delta;
+            rho0 = rho1;
+        }
+        return cheb_fused(c, out, acc, vdot, part, c1, c2, theta);
+    }
     double *dcur = c->dA, *dnext = c->dB;
     for (int it = 0; it < c->pdeg; ++it) {
         const double rho1 = 1.0 / (2.0 * sigma - rho0);
@@ -881,8 +973,8 @@ int gk_mgs_cycle_start(gk_ctx *c, double *beta) {
     CHK(check_ctx(c));
     HIPCHK(hipSetDevice(c->dev));
     CHK(op_precond(c, c->x, c->w, true, gk::ACC_NORM, nullptr, slot(c, 0)));
-    CHK(allreduce(c, slot(c, 0), c->np_st));
-    CHK(scale(c, c->V, c->w, slot(c, 0), c->np_st, c->hcol));
+    CHK(allreduce(c, slot(c, 0), c->last_np));
+    CHK(scale(c, c->V, c->w, slot(c, 0), c->last_np, c->hcol));
     CHK(d2h_sync(c, beta, c->hcol, 1));
     c->cycle_mgs = true;
     c->cycle_hh = false;
@@ -902,7 +994,7 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
     int s0 = 0, s1 = 1;
     // w = M^-1 A V(:,j), fused with the first dot <w, V(:,1)>
     CHK(op_precond(c, V + (i64)(j - 1) * ld, c->w, false, gk::ACC_DOT, V, slot(c, s0)));
-    int np = c->np_st;
+    int np = c->last_np;
     // two MGS passes: projection p = (k, i), AXPY of p fused with the dot of p+1
     const int np_total = 2 * j;
     for (int p = 0; p < np_total; ++p) {
@@ -1013,11 +1105,11 @@ int gk_hh_cycle_start(gk_ctx *c, int precondition, double *g1) {
         a.part = slot(c, 0);
         CHK(stencil(c, gk::OP_RESID, gk::ACC_NORM, a));
     }
-    CHK(allreduce(c, slot(c, 0), c->np_st));
+    CHK(allreduce(c, slot(c, 0), c->last_np));
     CHK(hh_pivot(c, 0, nullptr, 0));
     {
         ProfScope ps(c, GK_KID_OTHER);
-        gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, 0), c->np_st, 0, c->hcol, c->scal + 2);
+        gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, 0), c->last_np, 0, c->hcol, c->scal + 2);
         LAUNCHCHK();
         // w(1) = sign(beta,w(1)) + w(1); norm2(w)
         gk::k_hh_fix<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->w, c->nloc, c->g0, 0, 0, c->scal + 2, slot(c, 1));
@@ -1058,7 +1150,7 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
         a.part = slot(c, s0);
         CHK(stencil(c, gk::OP_PLAIN, gk::ACC_DOT, a));
     }
-    int np = c->np_st;
+    int np = c->last_np;
     // w = P_j .. P_1 w ; the last reflection also accumulates ||w(j+1:n)||^2
     for (int i = 1; i <= j; ++i) {
         CHK(allreduce(c, slot(c, s0), np));
@@ -1180,6 +1272,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_PROJ_BLOCKS: c->tune_pj_blocks = value; break;
         case GK_TUNE_STENCIL_BLOCKS: c->tune_st_blocks = value; break;
         case GK_TUNE_PROJ_REV: c->tune_rev = value != 0; break;
+        case GK_TUNE_CHEB_FUSED: c->tune_cheb_fused = value != 0; break;
         case GK_TUNE_PROJ_BLOCKED: c->tune_blocked = value != 0; break;
         case GK_TUNE_PROJ_UNROLL:
             if (value != 0 && value != 2 && value != 4 && value != 8)

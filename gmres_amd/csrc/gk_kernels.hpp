@@ -602,3 +602,148 @@ __global__ __launch_bounds__(TPB) void k_gram_reduce(const double *__restrict__ 
 }
 
 }  // namespace gk
+
+namespace gk {
+
+// --------------------------------------------------------------------------
+// Temporal blocking of the Chebyshev(k) sweeps (single slab): L sweeps of
+//   res' = res - A d ;  d' = c1 d + c2 res' ;  z' = z + d'
+// in ONE pass.  A workgroup is one wave owning a 128-point window of the fast
+// index i (an L-point halo each side is recomputed, 128 - 2L points are kept)
+// and marching down grid lines with an L-level register pipeline: each time
+// step one input line enters; level l consumes the line level l-1 emitted in
+// the same step, keeps a 3-line window of d plus the (res, z) of its middle
+// line, and emits its middle line.  Per point the arithmetic is exactly the
+// per-sweep kernel's (bit-identical), only the schedule differs: the group
+// moves ~3 vectors in and 3 out instead of 6 per sweep.
+// --------------------------------------------------------------------------
+constexpr int CF_W = 64;           // lanes per window (one wave)
+constexpr int CF_PTS = CF_W * 2;   // points per window (2 per lane)
+constexpr int CF_LMAX = 4;
+
+struct CFArgs {
+    const double *din;   // FIRST: z (the residual r); else d entering the group
+    const double *rin;   // !FIRST: residual entering the group
+    const double *zin;   // !FIRST: running sum entering the group
+    double *dout, *rout, *zout;  // !LAST outputs
+    double *out;         // LAST output (the preconditioned vector)
+    const double *vdot;  // ACC_DOT partner
+    double *part;
+    double theta;        // FIRST: d0 = r / theta
+    double c1[CF_LMAX], c2[CF_LMAX];
+    int N, nlines, JT;
+};
+
+template <int L, bool FIRST, bool LAST, int ACC>
+__global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
+    constexpr int H = L + (L & 1);                  // halo, even so a lane's 2 points are kept together
+    const int N = a.N;
+    const int lane = threadIdx.x;
+    const int keep = CF_PTS - 2 * H;
+    const i64 ob = (i64)blockIdx.x * keep;          // first kept point
+    const i64 i0 = ob - H + 2 * lane;               // this lane's points i0, i0+1 (i0 even, N even)
+    const bool in0 = i0 >= 0 && i0 < N, in1 = i0 + 1 >= 0 && i0 + 1 < N;
+    const bool kept = (2 * lane >= H) && (2 * lane < CF_PTS - H) && i0 < N;
+    const int j0 = blockIdx.y * a.JT;
+    const int j1 = min(j0 + a.JT, a.nlines);
+    double acc = 0.0;
+    // per-level state: 3-line window of d, (res, z) of the middle and newest lines
+    double dw[L][3][2], rm[L][2], zm[L][2], rn[L][2], zn[L][2];
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            dw[l][0][k] = dw[l][1][k] = dw[l][2][k] = 0.0;
+            rm[l][k] = zm[l][k] = rn[l][k] = zn[l][k] = 0.0;
+        }
+    auto ld2 = [&](const double *base, int row, double (&v)[2]) {
+        v[0] = v[1] = 0.0;
+        if (row < 0 || row >= a.nlines) return;
+        const double *p = base + (i64)row * N + i0;
+        if (in0 && in1) {
+            const double2 t = *reinterpret_cast<const double2 *>(p);
+            v[0] = t.x;
+            v[1] = t.y;
+        }
+    };
+    if (j0 < a.nlines) {
+        for (int t = j0 - L - 1; t < j1 + L; ++t) {
+            // emission of "level -1": the input line t
+            double ed[2], er[2], ez[2];
+            if (FIRST) {
+                double raw[2];
+                ld2(a.din, t, raw);
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    ed[k] = raw[k] / a.theta;
+                    er[k] = raw[k];
+                    ez[k] = ed[k];
+                }
+            } else {
+                ld2(a.din, t, ed);
+                ld2(a.rin, t, er);
+                ld2(a.zin, t, ez);
+            }
+            int row = t;  // row of the current emission
+#pragma unroll
+            for (int l = 0; l < L; ++l) {
+                // push the emission into level l
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    dw[l][0][k] = dw[l][1][k];
+                    dw[l][1][k] = dw[l][2][k];
+                    dw[l][2][k] = ed[k];
+                    rm[l][k] = rn[l][k];
+                    zm[l][k] = zn[l][k];
+                    rn[l][k] = er[k];
+                    zn[l][k] = ez[k];
+                }
+                // compute the middle line row-1
+                const int mrow = row - 1;
+                double left = __shfl_up(dw[l][1][1], 1, 64);
+                double right = __shfl_down(dw[l][1][0], 1, 64);
+                const bool rowok = mrow >= 0 && mrow < a.nlines;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const double W = (k == 0) ? left : dw[l][1][0];
+                    const double E = (k == 1) ? right : dw[l][1][1];
+                    const double s = ((W + E) + dw[l][2][k]) + dw[l][0][k];
+                    const double ad = 4.0 * dw[l][1][k] - 1.0 * s;
+                    const double res = rm[l][k] - ad;
+                    const double dn = a.c1[l] * dw[l][1][k] + a.c2[l] * res;
+                    const double z = zm[l][k] + dn;
+                    const bool ok = rowok && (k == 0 ? in0 : in1);
+                    ed[k] = ok ? dn : 0.0;
+                    er[k] = ok ? res : 0.0;
+                    ez[k] = ok ? z : 0.0;
+                }
+                row = mrow;
+            }
+            // the last level emitted line `row`
+            if (row >= j0 && row < j1 && kept) {
+                const i64 idx = (i64)row * N + i0;
+                if (LAST) {
+                    *reinterpret_cast<double2 *>(a.out + idx) = double2{ez[0], ez[1]};
+                    if (ACC == ACC_DOT) {
+                        const double2 v = *reinterpret_cast<const double2 *>(a.vdot + idx);
+                        acc = acc + ez[0] * v.x;
+                        acc = acc + ez[1] * v.y;
+                    } else if (ACC == ACC_NORM) {
+                        acc = acc + ez[0] * ez[0];
+                        acc = acc + ez[1] * ez[1];
+                    }
+                } else {
+                    *reinterpret_cast<double2 *>(a.dout + idx) = double2{ed[0], ed[1]};
+                    *reinterpret_cast<double2 *>(a.rout + idx) = double2{er[0], er[1]};
+                    *reinterpret_cast<double2 *>(a.zout + idx) = double2{ez[0], ez[1]};
+                }
+            }
+        }
+    }
+    if (ACC != ACC_NONE) {
+        const double s = wave_sum(acc);
+        if (lane == 0) a.part[(i64)blockIdx.y * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+}  // namespace gk

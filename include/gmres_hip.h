@@ -187,13 +187,16 @@ int gk_sync(gk_ctx *ctx);
  *   GK_TUNE_PROJ_REV       1: alternate the traversal direction of successive
  *                          projection launches (Infinity Cache reuse)
  *   GK_TUNE_PROJ_BLOCKED   1: contiguous range per workgroup; 0: grid-stride
- *   GK_TUNE_PROJ_UNROLL    double2 loads in flight per thread and array: 2, 4, 8; 0 = auto */
+ *   GK_TUNE_PROJ_UNROLL    double2 loads in flight per thread and array: 2, 4, 8; 0 = auto
+ *   GK_TUNE_CHEB_FUSED     1 (default): Chebyshev(k <= 8) as temporal-blocked passes of up to
+ *                          4 sweeps each (single slab, even N); 0: one launch per sweep */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
 #define GK_TUNE_PROJ_REV 3
 #define GK_TUNE_PROJ_BLOCKED 4
 #define GK_TUNE_PROJ_UNROLL 5
+#define GK_TUNE_CHEB_FUSED 6
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

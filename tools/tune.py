@@ -16,8 +16,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KEYS = {"nt": 0, "pj": 1, "st": 2, "rev": 3, "blk": 4, "unr": 5}
-DEFAULTS = {0: -1, 1: 0, 2: 0, 3: 0, 4: 0, 5: 0}
+KEYS = {"nt": 0, "pj": 1, "st": 2, "rev": 3, "blk": 4, "unr": 5, "cf": 6}
+DEFAULTS = {0: -1, 1: 0, 2: 0, 3: 0, 4: 0, 5: 0, 6: 1}
 
 
 def parse_variant(s: str) -> dict:
@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--grid", type=int, default=4096)
     ap.add_argument("--m", type=int, default=95)
     ap.add_argument("--prec", default="identity")
+    ap.add_argument("--degree", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", nargs="+", default=["base", "nt=1"])
     ap.add_argument("--out", default="")
@@ -42,7 +43,7 @@ def main():
     import gmres_amd as ga
 
     ctx = ga.Context(a.grid, a.m)
-    ctx.set_precond(a.prec)
+    ctx.set_precond(a.prec, (8.2, 0.2), a.degree)
     ctx.set_rhs_ones()
     ga.gmres_mgsr(ctx, 1e-15, max_cycles=1, want_verr=False)  # warm
     res = {v: {"wall_ms": [], "proj_us": [], "resid": None} for v in a.variants}
