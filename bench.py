@@ -94,6 +94,36 @@ def cpu_baseline(N: int, m: int, prec: str, degree: int, sample_steps: int, thre
                       f"cycle by the SURVEY 8(d) byte model"}
 
 
+def setup_xgmi(ctx, dist, world: int, rank: int, required: bool):
+    """Map every rank's exchange region (IPC handles over the gloo control
+    plane) and run the collective self-test; every rank must pass, else all
+    ranks fall back to RCCL (or fail when --collective xgmi was asked for)."""
+    import torch
+
+    ok = 1
+    hs = [None] * world
+    try:
+        h = ctx.xchg_handle()
+        dist.all_gather_object(hs, h)
+        ctx.xchg_open(hs)
+    except Exception as e:  # noqa: BLE001 - reported, then the self-test decides
+        print(f"rank {rank}: device exchange unavailable: {e}", file=sys.stderr)
+        ok = 0
+    if ok:
+        ok = int(ctx.xchg_selftest(5000))
+        if not ok:
+            print(f"rank {rank}: {getattr(ctx, 'xchg_error', '')}", file=sys.stderr)
+    t = torch.tensor([ok], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if int(t.item()) == 1:
+        return "xgmi-device-exchange"
+    if required:
+        raise RuntimeError("--collective xgmi: device exchange self-test failed")
+    if ok:
+        ctx.xchg_enable(False)
+    return None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,6 +138,9 @@ def main() -> None:
     ap.add_argument("--cpu-steps", type=int, default=90)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-prof", action="store_true", help="no HIP-event kernel timing in the timed region")
+    ap.add_argument("--collective", default="auto", choices=["auto", "rccl", "xgmi"],
+                    help="N>1: RCCL calls, or the device exchange over xGMI (auto: device exchange if its "
+                         "self-test passes on every rank, else RCCL)")
     ap.add_argument("--prof-every", type=int, default=16,
                     help="HIP events around the launches of every S-th Arnoldi step (1 = all)")
     args = ap.parse_args()
@@ -131,11 +164,18 @@ def main() -> None:
     parts = ga.slab_partition(N, world)
     line0, nlines = parts[rank]
     ctx = ga.Context(N, m, device=local, line0=line0, nlines=nlines)
-    if world > 1 or os.environ.get("GK_FORCE_RCCL") == "1":  # 1-rank RCCL: exercises the comm path
+    ml = max(p[1] for p in parts)
+    collective = None
+    if world > 1 and args.collective == "xgmi":
+        ctx.comm_init_xgmi(world, rank, ml)
+    elif world > 1 or os.environ.get("GK_FORCE_RCCL") == "1":  # 1-rank RCCL: exercises the comm path
         obj = [ga.Context.unique_id() if rank == 0 else None]
         if dist is not None:
             dist.broadcast_object_list(obj, src=0)
-        ctx.comm_init(world, rank, max(p[1] for p in parts), obj[0])
+        ctx.comm_init(world, rank, ml, obj[0])
+        collective = "rccl"
+    if world > 1 and args.collective in ("auto", "xgmi"):
+        collective = setup_xgmi(ctx, dist, world, rank, required=args.collective == "xgmi") or "rccl"
     ctx.set_precond(args.prec, (8.2, 0.2), args.degree)
     ctx.set_rhs_ones()
 
@@ -162,6 +202,7 @@ def main() -> None:
     barrier()
     t1 = time.perf_counter()
     prof = ctx.profile_read() if not args.no_prof else {}
+    resid = ctx.true_residual()  # outside the timed region; same value at any N
     elapsed = t1 - t0
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -234,7 +275,8 @@ def main() -> None:
             "config": {"workload": f"{N}x{N} Poisson-2D fp64, GMRES-{args.method.upper()} m={m}, {prec_name}",
                        "grid": N, "m": m, "precond": args.prec, "method": args.method,
                        "step": "one GMRES(m) restart cycle", "parallelism": f"row-block slabs x{world}",
-                       "arnoldi_iters": iters},
+                       "collective": collective, "arnoldi_iters": iters},
+            "check": {"true_rel_residual_after_timed_cycles": resid},
             "hbm_gbps_alg": round(gbps_alg, 1) if gbps_alg else None,
             "cycle_roofline_frac": round(gbps_alg / HBM_PEAK_GBPS, 4) if gbps_alg else None,
             "roofline": roof,

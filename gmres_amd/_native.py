@@ -19,6 +19,8 @@ FHOST_SO = os.path.join(LIB_DIR, "libgmres_fhost.so")
 HEADER = os.path.join(os.path.dirname(PKG), "include", "gmres_hip.h")
 
 GK_OK = 0
+GK_ERR_COMM = -6
+GK_TUNE_XCHG_TIMEOUT_MS = 7
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER = range(6)
 KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other"]
@@ -52,6 +54,12 @@ _SIGS = {
     "gk_group_create": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "gk_group_destroy": (c_int, [c_vp]),
     "gk_comm_init_local": (c_int, [c_vp, c_vp, c_int, c_int]),
+    "gk_comm_init_xgmi": (c_int, [c_vp, c_int, c_int, c_int]),
+    "gk_xchg_handle": (c_int, [c_vp, ctypes.c_char_p]),
+    "gk_xchg_open": (c_int, [c_vp, ctypes.c_char_p]),
+    "gk_xchg_local": (c_int, [c_vp]),
+    "gk_xchg_enable": (c_int, [c_vp, c_int]),
+    "gk_xchg_selftest": (c_int, [c_vp, c_int]),
     "gk_set_precond": (c_int, [c_vp, c_int, _dp, c_int, c_int]),
     "gk_set_rhs": (c_int, [c_vp, _dp]),
     "gk_set_rhs_ones": (c_int, [c_vp]),
@@ -129,6 +137,11 @@ def fhost() -> ctypes.CDLL:
             f.argtypes = args
         _fhost = L
     return _fhost
+
+
+def last_error() -> str:
+    msg = hip().gk_last_error()
+    return msg.decode() if msg else ""
 
 
 def check(status: int, what: str) -> None:

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -113,6 +114,17 @@ struct gk_ctx {
     gk_group *lg = nullptr;  // in-process group (GK local comm), else RCCL
     hipEvent_t lev_a = nullptr, lev_b = nullptr;
     double *lscratch = nullptr;
+    // device exchange (xgmi back-end, gk_comm_init_xgmi / gk_xchg_*)
+    gk::u64 *xs_buf = nullptr;  // own receive region, uncached HBM
+    i64 xs_words = 0;
+    gk::XsPeers xs_peers{};     // every rank's region, mapped here
+    std::vector<void *> xs_mapped;
+    bool xs_ready = false, xs_on = false;
+    unsigned xs_seq = 0, xs_hseq = 0;
+    int *xs_err = nullptr, *xs_err_dev = nullptr;  // mapped pinned flag
+    long long xs_tick_per_ms = 100000;
+    int xs_timeout_ms = 20000;
+    gk::u64 xs_timeout = 0;
     // launch geometry
     int vec = 2, JT = 16;
     dim3 sgrid;
@@ -185,7 +197,65 @@ __global__ void k_sum_ranks(RankPtrs src, int nr, double *__restrict__ out, int 
 }
 
 // Collectives run whenever a communicator exists (also a 1-rank RCCL one).
-bool collective(const gk_ctx *c) { return c->comm != nullptr || c->lg != nullptr; }
+bool collective(const gk_ctx *c) { return c->xs_on || c->comm != nullptr || c->lg != nullptr; }
+
+// ------------------------------------------------ device exchange (xgmi) ---
+void xs_set_timeout(gk_ctx *c, int ms) {
+    c->xs_timeout_ms = ms;
+    c->xs_timeout = (gk::u64)ms * (gk::u64)c->xs_tick_per_ms;
+}
+
+int xs_alloc(gk_ctx *c) {
+    if (c->xs_buf != nullptr) return GK_OK;
+    HIPCHK(hipSetDevice(c->dev));
+    c->xs_words = gk::XS_RED_WORDS + 8LL * c->N;
+    if (hipExtMallocWithFlags((void **)&c->xs_buf, sizeof(gk::u64) * c->xs_words, hipDeviceMallocUncached) !=
+        hipSuccess)
+        return set_err(GK_ERR_NOMEM, "cannot allocate the exchange region");
+    HIPCHK(hipMemsetAsync(c->xs_buf, 0, sizeof(gk::u64) * c->xs_words, c->st));
+    HIPCHK(hipHostMalloc((void **)&c->xs_err, sizeof(int), hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer((void **)&c->xs_err_dev, c->xs_err, 0));
+    *c->xs_err = 0;
+    int khz = 0;
+    HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev));
+    if (khz > 0) c->xs_tick_per_ms = khz;
+    xs_set_timeout(c, c->xs_timeout_ms);
+    HIPCHK(hipStreamSynchronize(c->st));  // zeroed before any peer can see the region
+    return GK_OK;
+}
+
+// After a host wait: did a device exchange miss its deadline?
+int xs_check(gk_ctx *c) {
+    if (c->xs_err != nullptr && __atomic_load_n(c->xs_err, __ATOMIC_ACQUIRE) != 0)
+        return set_err(GK_ERR_COMM, "device exchange: a peer missed the %d ms deadline (rank %d of %d)",
+                       c->xs_timeout_ms, c->rank, c->nranks);
+    return GK_OK;
+}
+
+int sync_st(gk_ctx *c) {
+    HIPCHK(hipStreamSynchronize(c->st));
+    return xs_check(c);
+}
+
+int xs_exchange(gk_ctx *c, double *buf, int count, int mode, int root) {
+    const unsigned seq = ++c->xs_seq;
+    switch (mode) {
+        case gk::XS_SLAB:
+            gk::k_xchg<gk::XS_SLAB><<<1, gk::TPB, 0, c->st>>>(buf, count, c->xs_peers, c->nranks, c->rank, seq, root,
+                                                            c->xs_err_dev, c->xs_timeout);
+            break;
+        case gk::XS_VEC:
+            gk::k_xchg<gk::XS_VEC><<<1, gk::TPB, 0, c->st>>>(buf, count, c->xs_peers, c->nranks, c->rank, seq, root,
+                                                           c->xs_err_dev, c->xs_timeout);
+            break;
+        default:
+            gk::k_xchg<gk::XS_BCAST><<<1, gk::TPB, 0, c->st>>>(buf, count, c->xs_peers, c->nranks, c->rank, seq,
+                                                             root, c->xs_err_dev, c->xs_timeout);
+            break;
+    }
+    LAUNCHCHK();
+    return GK_OK;
+}
 
 int lg_barrier(gk_ctx *c) {
     gk_group *g = c->lg;
@@ -219,9 +289,17 @@ int lg_wait(gk_ctx *c, int q, bool second) {
     return GK_OK;
 }
 
-int allreduce(gk_ctx *c, double *buf, int count) {
+// `vec`: element-wise sum of a short vector; otherwise `buf` is a partial slab
+// whose consumer re-reduces it (any split of the same total is equivalent).
+int allreduce(gk_ctx *c, double *buf, int count, bool vec = false) {
     if (!collective(c)) return GK_OK;
     ProfScope ps(c, GK_KID_COMM);
+    if (c->xs_on) {
+        if (!vec) return xs_exchange(c, buf, count, gk::XS_SLAB, 0);
+        for (int k0 = 0; k0 < count; k0 += gk::XS_MAXV)
+            CHK(xs_exchange(c, buf + k0, std::min(gk::XS_MAXV, count - k0), gk::XS_VEC, 0));
+        return GK_OK;
+    }
     if (c->lg == nullptr) {
         NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->st));
         return GK_OK;
@@ -245,6 +323,11 @@ int allreduce(gk_ctx *c, double *buf, int count) {
 int bcast(gk_ctx *c, double *buf, int count, int root) {
     if (!collective(c)) return GK_OK;
     ProfScope ps(c, GK_KID_COMM);
+    if (c->xs_on) {
+        for (int k0 = 0; k0 < count; k0 += gk::XS_MAXV)
+            CHK(xs_exchange(c, buf + k0, std::min(gk::XS_MAXV, count - k0), gk::XS_BCAST, root));
+        return GK_OK;
+    }
     if (c->lg == nullptr) {
         NCCLCHK(ncclBroadcast(buf, buf, count, ncclDouble, root, c->comm, c->st));
         return GK_OK;
@@ -266,6 +349,15 @@ int halo(gk_ctx *c, const double *vec) {
     if (!collective(c)) return GK_OK;
     ProfScope ps(c, GK_KID_COMM);
     const int N = c->N;
+    if (c->xs_on) {
+        if (c->nranks == 1) return GK_OK;
+        const unsigned seq = ++c->xs_hseq;
+        gk::k_xhalo<<<(N + gk::TPB - 1) / gk::TPB, gk::TPB, 0, c->st>>>(vec, N, c->nlines, c->xs_peers, c->nranks,
+                                                                       c->rank, seq, c->hlo, c->hhi, c->xs_err_dev,
+                                                                       c->xs_timeout);
+        LAUNCHCHK();
+        return GK_OK;
+    }
     if (c->lg == nullptr) {
         NCCLCHK(ncclGroupStart());
         if (c->rank > 0) {
@@ -446,7 +538,7 @@ int finalize(gk_ctx *c, const double *pin, int npin, double *out, int take_sqrt)
 
 int d2h_sync(gk_ctx *c, double *host, const double *dev, int count) {
     HIPCHK(hipMemcpyAsync(c->hcol_host, dev, sizeof(double) * count, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     if (c->prof) CHK(prof_harvest(c));
     std::memcpy(host, c->hcol_host, sizeof(double) * count);
     return GK_OK;
@@ -668,10 +760,10 @@ int gram(gk_ctx *c, const double *base, int ncols, std::vector<double> &G) {
                                                                             np, c->gram_out);
         LAUNCHCHK();
     }
-    CHK(allreduce(c, c->gram_out, np));
+    CHK(allreduce(c, c->gram_out, np, true));
     std::vector<double> flat(np);
     HIPCHK(hipMemcpyAsync(flat.data(), c->gram_out, sizeof(double) * np, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     if (c->prof) CHK(prof_harvest(c));
     G.assign((size_t)ncols * ncols, 0.0);
     for (int p = 0; p < np; ++p) {
@@ -782,6 +874,9 @@ int gk_destroy(gk_ctx *c) {
     if (c->lev_a) (void)hipEventDestroy(c->lev_a);
     if (c->lev_b) (void)hipEventDestroy(c->lev_b);
     if (c->lscratch) (void)hipFree(c->lscratch);
+    for (void *p : c->xs_mapped) (void)hipIpcCloseMemHandle(p);
+    if (c->xs_buf) (void)hipFree(c->xs_buf);
+    if (c->xs_err) (void)hipHostFree(c->xs_err);
     double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi,
                       c->red, c->hcol, c->ydev, c->hb, c->scal, c->Vb, c->gram_slab, c->gram_out};
     for (double *p : bufs)
@@ -861,7 +956,159 @@ int gk_comm_init_local(gk_ctx *c, gk_group *g, int rank, int max_lines) {
         std::lock_guard<std::mutex> lk(g->mu);
         g->members[rank] = c;
     }
+    CHK(xs_alloc(c));
     c->comm_ok = true;
+    return GK_OK;
+}
+
+int gk_comm_init_xgmi(gk_ctx *c, int nranks, int rank, int max_lines) {
+    if (c == nullptr || nranks < 1 || nranks > gk::XS_MAXR || rank < 0 || rank >= nranks || max_lines < c->nlines)
+        return set_err(GK_ERR_ARG, "bad xgmi comm args (nranks <= %d)", gk::XS_MAXR);
+    HIPCHK(hipSetDevice(c->dev));
+    c->nranks = nranks;
+    c->rank = rank;
+    c->max_lines = max_lines;
+    set_geometry(c);
+    return xs_alloc(c);  // comm_ok once gk_xchg_open has mapped the peers
+}
+
+int gk_xchg_handle(gk_ctx *c, unsigned char handle[64]) {
+    if (c == nullptr || handle == nullptr) return set_err(GK_ERR_ARG, "null argument");
+    CHK(xs_alloc(c));
+    hipIpcMemHandle_t h;
+    static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t size");
+    HIPCHK(hipIpcGetMemHandle(&h, c->xs_buf));
+    std::memcpy(handle, &h, 64);
+    return GK_OK;
+}
+
+int gk_xchg_open(gk_ctx *c, const unsigned char *handles) {
+    if (c == nullptr || handles == nullptr) return set_err(GK_ERR_ARG, "null argument");
+    if (c->nranks > gk::XS_MAXR) return set_err(GK_ERR_ARG, "device exchange supports <= %d ranks", gk::XS_MAXR);
+    if (c->xs_ready) return set_err(GK_ERR_STATE, "exchange already open");
+    CHK(xs_alloc(c));
+    HIPCHK(hipSetDevice(c->dev));
+    for (int r = 0; r < c->nranks; ++r) {
+        if (r == c->rank) {
+            c->xs_peers.p[r] = c->xs_buf;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + 64 * (size_t)r, 64);
+        void *p = nullptr;
+        HIPCHK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        c->xs_mapped.push_back(p);
+        c->xs_peers.p[r] = static_cast<gk::u64 *>(p);
+    }
+    c->xs_ready = true;
+    c->xs_on = true;
+    c->comm_ok = true;
+    return GK_OK;
+}
+
+int gk_xchg_local(gk_ctx *c) {
+    if (c == nullptr || c->lg == nullptr) return set_err(GK_ERR_STATE, "gk_xchg_local needs gk_comm_init_local");
+    if (c->nranks > gk::XS_MAXR) return set_err(GK_ERR_ARG, "device exchange supports <= %d ranks", gk::XS_MAXR);
+    std::lock_guard<std::mutex> lk(c->lg->mu);
+    for (int r = 0; r < c->nranks; ++r) {
+        gk_ctx *o = c->lg->members[r];
+        if (o == nullptr || o->xs_buf == nullptr)
+            return set_err(GK_ERR_STATE, "rank %d of the group has not joined yet", r);
+        c->xs_peers.p[r] = o->xs_buf;
+    }
+    c->xs_ready = true;
+    c->xs_on = true;
+    return GK_OK;
+}
+
+int gk_xchg_enable(gk_ctx *c, int on) {
+    if (c == nullptr) return set_err(GK_ERR_ARG, "null context");
+    if (on && !c->xs_ready) return set_err(GK_ERR_STATE, "exchange not open");
+    if (!on && c->comm == nullptr && c->lg == nullptr && c->nranks > 1)
+        return set_err(GK_ERR_STATE, "no RCCL or local communicator to fall back to");
+    c->xs_on = on != 0;
+    return GK_OK;
+}
+
+namespace {
+double host_hash(long long g, unsigned long long seed) {  // = gk::k_fill_hash
+    unsigned long long z = (unsigned long long)g + seed * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z = z ^ (z >> 31);
+    return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
+int xs_selftest_body(gk_ctx *c, std::string &why) {
+    const int R = c->nranks, me = c->rank;
+    // element-wise sum of a short vector
+    double hv[8];
+    for (int k = 0; k < 8; ++k) hv[k] = (me + 1) * (k + 1) + 0.25 * k;
+    double *d = slot(c, 3);
+    HIPCHK(hipMemcpyAsync(d, hv, sizeof hv, hipMemcpyHostToDevice, c->st));
+    CHK(allreduce(c, d, 8, true));
+    // a partial slab: 5 partials of (rank+1) -> {5 * sum(rank+1), 0, 0, 0, 0}
+    double hs[5];
+    for (double &v : hs) v = me + 1.0;
+    double *e = slot(c, 2);
+    HIPCHK(hipMemcpyAsync(e, hs, sizeof hs, hipMemcpyHostToDevice, c->st));
+    CHK(allreduce(c, e, 5));
+    // broadcast from the last rank
+    double hb[3] = {me + 0.5, -me - 0.5, 1e300 * (me + 1)};
+    HIPCHK(hipMemcpyAsync(c->hb, hb, sizeof hb, hipMemcpyHostToDevice, c->st));
+    CHK(bcast(c, c->hb, 3, R - 1));
+    // halo lines of a globally indexed vector
+    gk::k_fill_hash<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->vj, c->nloc, c->g0, 7);
+    LAUNCHCHK();
+    CHK(halo(c, c->vj));
+    double rv[8], rs[5], rb[3];
+    std::vector<double> lo(c->N), hi(c->N);
+    HIPCHK(hipMemcpyAsync(rv, d, sizeof rv, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(rs, e, sizeof rs, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(rb, c->hb, sizeof rb, hipMemcpyDeviceToHost, c->st));
+    if (me > 0) HIPCHK(hipMemcpyAsync(lo.data(), c->hlo, sizeof(double) * c->N, hipMemcpyDeviceToHost, c->st));
+    if (me < R - 1) HIPCHK(hipMemcpyAsync(hi.data(), c->hhi, sizeof(double) * c->N, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (*c->xs_err) {
+        why = "a peer missed the deadline";
+        return GK_ERR_COMM;
+    }
+    for (int k = 0; k < 8; ++k) {
+        double ex = 0.0;
+        for (int r = 0; r < R; ++r) ex = ex + ((r + 1) * (k + 1) + 0.25 * k);
+        if (rv[k] != ex) why = "vector all-reduce mismatch";
+    }
+    if (rs[0] != 5.0 * (R * (R + 1) / 2) || rs[1] != 0.0 || rs[4] != 0.0) why = "slab all-reduce mismatch";
+    const int rt = R - 1;
+    if (rb[0] != rt + 0.5 || rb[1] != -rt - 0.5 || rb[2] != 1e300 * (rt + 1)) why = "broadcast mismatch";
+    for (int i = 0; i < c->N; ++i) {
+        if (me > 0 && lo[i] != host_hash(c->g0 - c->N + i, 7)) why = "lower halo mismatch";
+        if (me < R - 1 && hi[i] != host_hash(c->g0 + c->nloc + i, 7)) why = "upper halo mismatch";
+    }
+    return why.empty() ? GK_OK : GK_ERR_COMM;
+}
+}  // namespace
+
+int gk_xchg_selftest(gk_ctx *c, int timeout_ms) {
+    CHK(check_ctx(c));
+    if (!c->xs_ready) return set_err(GK_ERR_STATE, "exchange not open");
+    HIPCHK(hipSetDevice(c->dev));
+    const bool was_on = c->xs_on;
+    const int t_keep = c->xs_timeout_ms;
+    c->xs_on = true;
+    xs_set_timeout(c, timeout_ms > 0 ? timeout_ms : t_keep);
+    std::string why;
+    int rc = xs_selftest_body(c, why);
+    if (rc == GK_ERR_HIP || rc == GK_ERR_ARG) why = g_err;
+    xs_set_timeout(c, t_keep);
+    if (rc != GK_OK) {
+        (void)hipStreamSynchronize(c->st);
+        *c->xs_err = 0;
+        c->xs_on = false;
+        if (c->comm == nullptr && c->lg == nullptr) c->comm_ok = c->nranks == 1;
+        return set_err(GK_ERR_COMM, "device exchange self-test failed on rank %d: %s", c->rank, why.c_str());
+    }
+    (void)was_on;
     return GK_OK;
 }
 
@@ -892,7 +1139,7 @@ int gk_set_rhs(gk_ctx *c, const double *b) {
     CHK(check_ctx(c));
     HIPCHK(hipSetDevice(c->dev));
     HIPCHK(hipMemcpyAsync(c->b, b, sizeof(double) * c->nloc, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     c->beta0 = -1.0;
     return GK_OK;
 }
@@ -907,7 +1154,7 @@ int gk_set_rhs_ones(gk_ctx *c) {
     a.x = c->aux;
     a.y = c->b;
     CHK(stencil(c, gk::OP_PLAIN, gk::ACC_NONE, a));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     c->beta0 = -1.0;
     return GK_OK;
 }
@@ -927,7 +1174,7 @@ int gk_zero_x(gk_ctx *c) {
     CHK(check_ctx(c));
     HIPCHK(hipSetDevice(c->dev));
     HIPCHK(hipMemsetAsync(c->x, 0, sizeof(double) * c->nloc, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     return GK_OK;
 }
 
@@ -935,7 +1182,7 @@ int gk_get_x(gk_ctx *c, double *x) {
     CHK(check_ctx(c));
     HIPCHK(hipSetDevice(c->dev));
     HIPCHK(hipMemcpyAsync(x, c->x, sizeof(double) * c->nloc, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     return GK_OK;
 }
 
@@ -943,7 +1190,7 @@ int gk_set_x(gk_ctx *c, const double *x) {
     CHK(check_ctx(c));
     HIPCHK(hipSetDevice(c->dev));
     HIPCHK(hipMemcpyAsync(c->x, x, sizeof(double) * c->nloc, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     return GK_OK;
 }
 
@@ -1024,6 +1271,7 @@ int gk_mgs_step_wait(gk_ctx *c, int j, double *hcol) {
     CHK(check_ctx(c));
     if (j < 1 || j > c->m) return set_err(GK_ERR_ARG, "step j=%d outside 1..%d", j, c->m);
     HIPCHK(hipEventSynchronize(c->ev_step[j]));
+    CHK(xs_check(c));
     const volatile double *src = c->hallh + (i64)(j - 1) * (c->m + 2);
     for (int k = 0; k <= j; ++k) hcol[k] = src[k];
     return GK_OK;
@@ -1044,7 +1292,7 @@ int gk_update_x(gk_ctx *c, const double *y, int n_out) {
         gk::k_update_x<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->x, c->V, c->ld, c->ydev, n_out, c->nloc);
         LAUNCHCHK();
     }
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     if (c->prof) CHK(prof_harvest(c));
     return GK_OK;
 }
@@ -1206,7 +1454,7 @@ int gk_hh_update_x(gk_ctx *c, const double *y, int n_out) {
         gk::k_add<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->x, c->w, c->nloc);
         LAUNCHCHK();
     }
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     if (c->prof) CHK(prof_harvest(c));
     return GK_OK;
 }
@@ -1260,7 +1508,7 @@ int gk_apply(gk_ctx *c, int what, const double *in, double *out) {
         }
     }
     HIPCHK(hipMemcpyAsync(out, c->w, sizeof(double) * c->nloc, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     if (c->prof) CHK(prof_harvest(c));
     return GK_OK;
 }
@@ -1274,6 +1522,10 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_PROJ_REV: c->tune_rev = value != 0; break;
         case GK_TUNE_CHEB_FUSED: c->tune_cheb_fused = value != 0; break;
         case GK_TUNE_PROJ_BLOCKED: c->tune_blocked = value != 0; break;
+        case GK_TUNE_XCHG_TIMEOUT_MS:
+            if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
+            xs_set_timeout(c, value);
+            break;
         case GK_TUNE_PROJ_UNROLL:
             if (value != 0 && value != 2 && value != 4 && value != 8)
                 return set_err(GK_ERR_ARG, "unroll must be 0 (auto), 2, 4 or 8");
@@ -1318,7 +1570,7 @@ int gk_profile_read(gk_ctx *c, int kid, double *total_ms, long long *launches) {
 int gk_sync(gk_ctx *c) {
     CHK(check_ctx(c));
     HIPCHK(hipSetDevice(c->dev));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     if (c->prof) CHK(prof_harvest(c));
     return GK_OK;
 }
@@ -1522,7 +1774,7 @@ extern "C" int gk_lanczos_bounds(gk_ctx *c, int k, double *lmin, double *lmax) {
     be.resize(al.size() > 0 ? al.size() - 1 : 0);
     *lmin = tridiag_eig(al, be, 0);
     *lmax = tridiag_eig(al, be, (int)al.size() - 1);
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(sync_st(c));
     return GK_OK;
 }
 

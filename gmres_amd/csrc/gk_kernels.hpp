@@ -746,4 +746,170 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
     }
 }
 
+// --------------------------------------------------------------------------
+// Device-initiated exchange between ranks (the "xgmi" collective back-end).
+//
+// Every rank owns one receive region in uncached HBM that is mapped into every
+// peer (IPC handles across processes, plain pointers inside one process).  A
+// value travels as granules: one 8-byte word {32 data bits | 32-bit tag}
+// written by ONE system-scope 8-byte store, so a receiver that reads the tag of
+// the current exchange also reads its data -- no separate flag, no fence.
+// Slots are double-buffered by the parity of the exchange sequence number.
+// Every exchange is a rendezvous (each rank waits for the granules of every
+// rank it receives from), so no rank gets two exchanges ahead of a partner and
+// a slot is never overwritten before it has been read.  Every wait is bounded
+// by a wall-clock deadline: a missing peer sets the context's error flag
+// instead of hanging the GPU, and every later exchange returns NaN at once.
+//
+// Region layout (8-byte words):
+//   reductions  [parity 2][source rank XS_MAXR][value XS_MAXV][half 2]
+//   halo lines  [parity 2][side 2][N][half 2]   side 0: from rank-1, 1: from rank+1
+// --------------------------------------------------------------------------
+constexpr int XS_MAXR = 16;
+constexpr int XS_MAXV = 128;
+constexpr i64 XS_RED_WORDS = 2LL * XS_MAXR * XS_MAXV * 2;
+typedef unsigned long long u64;
+struct XsPeers {
+    u64 *p[XS_MAXR];
+};
+enum { XS_SLAB = 0, XS_VEC = 1, XS_BCAST = 2 };
+
+__device__ __forceinline__ void xs_put(u64 *q, unsigned seq, unsigned data) {
+    __hip_atomic_store(q, ((u64)seq << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Spin until the granule at q carries `seq`; false once the deadline passed.
+__device__ __forceinline__ bool xs_get(const u64 *q, unsigned seq, u64 deadline, unsigned *data) {
+    for (;;) {
+        const u64 g = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((unsigned)(g >> 32) == seq) {
+            *data = (unsigned)g;
+            return true;
+        }
+        if (wall_clock64() > deadline) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+__device__ __forceinline__ int xs_flag(const int *err) {
+    return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void xs_fail(int *err) {
+    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// All-reduce / broadcast of a short vector, one workgroup per rank.
+//   XS_SLAB : buf[0..count) is a partial slab; each rank reduces its own slab in a
+//             fixed order, the ranks' totals are summed in rank order, and the
+//             slab becomes {total, 0, ..., 0} (its consumer re-reduces it).
+//   XS_VEC  : element-wise sum over ranks in rank order, count <= XS_MAXV.
+//   XS_BCAST: buf = root's buf, count <= XS_MAXV.
+// The rank-order sum is the same instruction sequence on every rank, so the
+// replicated host loops see bit-identical scalars.
+template <int MODE>
+__global__ __launch_bounds__(TPB) void k_xchg(double *__restrict__ buf, int count, XsPeers peers, int nranks,
+                                               int rank, unsigned seq, int root, int *err, u64 timeout) {
+    __shared__ double sm[WAVES];
+    __shared__ double pay[XS_MAXV];
+    __shared__ unsigned rv[XS_MAXR * XS_MAXV * 2];
+    __shared__ int bad;
+    const int plen = MODE == XS_SLAB ? 1 : count;
+    if (threadIdx.x == 0) bad = xs_flag(err);
+    if (MODE == XS_SLAB) {
+        const double s = reduce_slab(buf, count, sm);  // synchronises the block
+        if (threadIdx.x == 0) pay[0] = s;
+    } else {
+        for (int k = threadIdx.x; k < plen; k += TPB) pay[k] = buf[k];
+    }
+    __syncthreads();
+    const unsigned par = seq & 1u;
+    const int tot = nranks * plen * 2;
+    if (!bad) {
+        for (int t = threadIdx.x; t < tot; t += TPB) {
+            const int half = t & 1, k = (t >> 1) % plen, dst = (t >> 1) / plen;
+            const u64 bits = (u64)__double_as_longlong(pay[k]);
+            xs_put(peers.p[dst] + (((i64)par * XS_MAXR + rank) * XS_MAXV + k) * 2 + half, seq,
+                   half ? (unsigned)(bits >> 32) : (unsigned)bits);
+        }
+        const u64 deadline = wall_clock64() + timeout;
+        const u64 *mine = peers.p[rank];
+        bool ok = true;
+        for (int t = threadIdx.x; t < tot && ok; t += TPB) {
+            const int half = t & 1, k = (t >> 1) % plen, src = (t >> 1) / plen;
+            unsigned d = 0;
+            ok = xs_get(mine + (((i64)par * XS_MAXR + src) * XS_MAXV + k) * 2 + half, seq, deadline, &d);
+            rv[(src * XS_MAXV + k) * 2 + half] = d;
+        }
+        if (!ok) bad = 1;
+    }
+    __syncthreads();
+    if (bad) {
+        if (threadIdx.x == 0) xs_fail(err);
+        for (int k = threadIdx.x; k < count; k += TPB) buf[k] = __builtin_nan("");
+        return;
+    }
+    auto val = [&](int r, int k) {
+        const u64 lo = rv[(r * XS_MAXV + k) * 2], hi = rv[(r * XS_MAXV + k) * 2 + 1];
+        return __longlong_as_double((long long)((hi << 32) | lo));
+    };
+    for (int k = threadIdx.x; k < count; k += TPB) {
+        if (MODE == XS_SLAB && k > 0) {
+            buf[k] = 0.0;
+            continue;
+        }
+        double s;
+        if (MODE == XS_BCAST) {
+            s = val(root, k);
+        } else {
+            s = val(0, k);
+            for (int r = 1; r < nranks; ++r) s = s + val(r, k);
+        }
+        buf[k] = s;
+    }
+}
+
+// Halo lines through the same regions: my first grid line goes to rank-1
+// (its side 1), my last to rank+1 (its side 0); then wait for mine and decode
+// them into hlo / hhi, the buffers the stencil reads.  One thread per point.
+__global__ __launch_bounds__(TPB) void k_xhalo(const double *__restrict__ vec, int N, int nlines, XsPeers peers,
+                                               int nranks, int rank, unsigned seq, double *__restrict__ hlo,
+                                               double *__restrict__ hhi, int *err, u64 timeout) {
+    const int e = blockIdx.x * TPB + threadIdx.x;
+    if (e >= N) return;
+    const bool lo = rank > 0, hi = rank < nranks - 1;
+    const unsigned par = seq & 1u;
+    auto slot = [&](u64 *base, int side) { return base + gk::XS_RED_WORDS + (((i64)par * 2 + side) * N + e) * 2; };
+    if (xs_flag(err)) {
+        if (lo) hlo[e] = __builtin_nan("");
+        if (hi) hhi[e] = __builtin_nan("");
+        return;
+    }
+    if (lo) {
+        const u64 bits = (u64)__double_as_longlong(vec[e]);
+        u64 *q = slot(peers.p[rank - 1], 1);
+        xs_put(q, seq, (unsigned)bits);
+        xs_put(q + 1, seq, (unsigned)(bits >> 32));
+    }
+    if (hi) {
+        const u64 bits = (u64)__double_as_longlong(vec[(i64)(nlines - 1) * N + e]);
+        u64 *q = slot(peers.p[rank + 1], 0);
+        xs_put(q, seq, (unsigned)bits);
+        xs_put(q + 1, seq, (unsigned)(bits >> 32));
+    }
+    const u64 deadline = wall_clock64() + timeout;
+    u64 *mine = peers.p[rank];
+    for (int side = 0; side < 2; ++side) {
+        if (side == 0 ? !lo : !hi) continue;
+        const u64 *q = slot(mine, side);
+        unsigned a = 0, b = 0;
+        double v = __builtin_nan("");
+        if (xs_get(q, seq, deadline, &a) && xs_get(q + 1, seq, deadline, &b))
+            v = __longlong_as_double((long long)(((u64)b << 32) | a));
+        else
+            xs_fail(err);
+        (side == 0 ? hlo : hhi)[e] = v;
+    }
+}
+
 }  // namespace gk

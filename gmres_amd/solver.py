@@ -136,6 +136,38 @@ class Context:
         self.nranks, self.rank = group.nranks, rank
         self._group = group  # keep alive
 
+    # --- device exchange ("xgmi" collective back-end, gmres_hip.h) ---
+    def comm_init_xgmi(self, nranks: int, rank: int, max_lines: int) -> None:
+        """Slab decomposition without RCCL; collectives by device exchange
+        once xchg_open() has mapped every rank's receive region."""
+        nat.check(nat.hip().gk_comm_init_xgmi(self._h, nranks, rank, max_lines), "gk_comm_init_xgmi")
+        self.nranks, self.rank = nranks, rank
+
+    def xchg_handle(self) -> bytes:
+        buf = ctypes.create_string_buffer(64)
+        nat.check(nat.hip().gk_xchg_handle(self._h, buf), "gk_xchg_handle")
+        return buf.raw
+
+    def xchg_open(self, handles: list[bytes]) -> None:
+        assert len(handles) == self.nranks and all(len(h) == 64 for h in handles)
+        nat.check(nat.hip().gk_xchg_open(self._h, b"".join(handles)), "gk_xchg_open")
+
+    def xchg_local(self) -> None:
+        nat.check(nat.hip().gk_xchg_local(self._h), "gk_xchg_local")
+
+    def xchg_enable(self, on: bool) -> None:
+        nat.check(nat.hip().gk_xchg_enable(self._h, int(bool(on))), "gk_xchg_enable")
+
+    def xchg_selftest(self, timeout_ms: int = 5000) -> bool:
+        """Collective self-test of the device exchange; False (and the
+        exchange disabled on this rank) when it fails."""
+        rc = nat.hip().gk_xchg_selftest(self._h, int(timeout_ms))
+        if rc == nat.GK_ERR_COMM:
+            self.xchg_error = nat.last_error()
+            return False
+        nat.check(rc, "gk_xchg_selftest")
+        return True
+
     # -- problem setup ---------------------------------------------------
     def set_precond(self, kind: str | int = "identity", params=(8.2, 0.2), degree: int = 8) -> None:
         k = PREC[kind] if isinstance(kind, str) else int(kind)

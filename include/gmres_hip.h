@@ -38,6 +38,7 @@ extern "C" {
 #define GK_ERR_RCCL (-3)  /* RCCL error */
 #define GK_ERR_STATE (-4) /* call out of order (e.g. step before cycle start) */
 #define GK_ERR_NOMEM (-5) /* device allocation failed */
+#define GK_ERR_COMM (-6)  /* device exchange: a peer missed its deadline (see gk_comm_init_xgmi) */
 
 /* Preconditioner kinds (the reference's `precond` plug-ins). */
 #define GK_PREC_IDENTITY 0 /* z = r ; config 1 "no precond"  */
@@ -49,7 +50,7 @@ extern "C" {
 #define GK_KID_STENCIL 1 /* Poisson-5 stencil sweeps incl. fused preconditioner sweeps */
 #define GK_KID_SCALE 2   /* normalisation V(:,j+1) = w / h */
 #define GK_KID_UPDATE 3  /* x += V y */
-#define GK_KID_COMM 4    /* RCCL all-reduce / halo / broadcast */
+#define GK_KID_COMM 4    /* all-reduce / halo / broadcast (RCCL or device exchange) */
 #define GK_KID_OTHER 5
 #define GK_NKID 6
 
@@ -76,6 +77,31 @@ int gk_comm_init(gk_ctx *ctx, int nranks, int rank, int max_lines, const unsigne
 int gk_group_create(int nranks, gk_group **out);
 int gk_group_destroy(gk_group *g);
 int gk_comm_init_local(gk_ctx *ctx, gk_group *g, int rank, int max_lines);
+/* Device exchange ("xgmi" back-end, SURVEY 8e "custom xGMI flag-based
+ * all-reduce"): the per-projection all-reduces, the Householder broadcast and
+ * the halo lines are moved by the GPUs themselves -- each rank stores tagged
+ * 8-byte granules straight into every peer's receive region over xGMI, and
+ * the consumer polls its own region -- instead of one RCCL call per
+ * reduction.  Same results on every rank (rank-order sums).
+ *   gk_comm_init_xgmi   decomposition without RCCL (ranks on distinct GPUs,
+ *                       or several processes on one GPU);
+ *   gk_xchg_handle      this rank's IPC handle (64 bytes) to share out of band;
+ *   gk_xchg_open        map every rank's region (handles: nranks x 64 bytes,
+ *                       rank order) and route collectives through it;
+ *   gk_xchg_local       the same for a gk_group (in-process, after every
+ *                       member's gk_comm_init_local);
+ *   gk_xchg_enable      0: back to RCCL / the local group, 1: device exchange;
+ *   gk_xchg_selftest    collective check of the reduction and halo paths with
+ *                       a deadline; GK_ERR_COMM if any granule is missing or
+ *                       wrong.  Also usable after gk_comm_init (RCCL present):
+ *                       a failed test leaves the exchange disabled.
+ * Usable together with gk_comm_init (then RCCL remains the fallback). */
+int gk_comm_init_xgmi(gk_ctx *ctx, int nranks, int rank, int max_lines);
+int gk_xchg_handle(gk_ctx *ctx, unsigned char handle[64]);
+int gk_xchg_open(gk_ctx *ctx, const unsigned char *handles);
+int gk_xchg_local(gk_ctx *ctx);
+int gk_xchg_enable(gk_ctx *ctx, int on);
+int gk_xchg_selftest(gk_ctx *ctx, int timeout_ms);
 int gk_local_size(gk_ctx *ctx, long long *nloc);
 
 /* Preconditioner: kind GK_PREC_*, params (cbpr2: params[0..1] as
@@ -189,7 +215,8 @@ int gk_sync(gk_ctx *ctx);
  *   GK_TUNE_PROJ_BLOCKED   1: contiguous range per workgroup; 0: grid-stride
  *   GK_TUNE_PROJ_UNROLL    double2 loads in flight per thread and array: 2, 4, 8; 0 = auto
  *   GK_TUNE_CHEB_FUSED     1 (default): Chebyshev(k <= 8) as temporal-blocked passes of up to
- *                          4 sweeps each (single slab, even N); 0: one launch per sweep */
+ *                          4 sweeps each (single slab, even N); 0: one launch per sweep
+ *   GK_TUNE_XCHG_TIMEOUT_MS deadline of one device-exchange wait (default 20000) */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
@@ -197,6 +224,7 @@ int gk_sync(gk_ctx *ctx);
 #define GK_TUNE_PROJ_BLOCKED 4
 #define GK_TUNE_PROJ_UNROLL 5
 #define GK_TUNE_CHEB_FUSED 6
+#define GK_TUNE_XCHG_TIMEOUT_MS 7
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

@@ -1,0 +1,212 @@
+"""Device-exchange collective back-end (include/gmres_hip.h gk_comm_init_xgmi /
+gk_xchg_*) on ONE GPU.
+
+The multi-GPU data path replaces the per-projection RCCL all-reduce, the
+Householder broadcast and the halo send/recv with stores of tagged 8-byte
+granules into every peer's receive region ("custom xGMI flag-based
+all-reduce").  A 1-GPU box cannot host two RCCL ranks, but it can host the
+device exchange: several contexts of one process (plain pointers), or several
+processes sharing the GPU through IPC handles -- the same code path the
+8-GPU run takes, minus the xGMI links.
+
+Results: every rank takes the same decisions (rank-order sums are
+bit-identical on all ranks) and the slab solve matches the single-context
+solve within the tolerances of test_gpu_multirank.py.
+"""
+import multiprocessing as mp
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _single(N, m, method, prec, degree, max_cycles):
+    import gmres_amd as ga
+
+    with ga.Context(N, m) as c:
+        c.set_precond(prec, (8.2, 0.2), degree)
+        c.set_rhs_ones()
+        return _solve(c, method, prec, max_cycles)
+
+
+def _solve(c, method, prec, max_cycles):
+    import gmres_amd as ga
+
+    if method == "mgsr":
+        return ga.gmres_mgsr(c, 1e-15, max_cycles=max_cycles, want_hist=True)
+    return ga.gmres_hh(c, 1e-15, precondition=(prec != "identity"), max_cycles=max_cycles, want_hist=True)
+
+
+def _run_threads(nranks, fn):
+    out, err = [None] * nranks, []
+
+    def work(r):
+        try:
+            out[r] = fn(r)
+        except Exception as e:  # pragma: no cover - reported below
+            err.append(e)
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not err, err
+    return out
+
+
+def _local_group(N, m, nranks):
+    import gmres_amd as ga
+
+    parts = ga.slab_partition(N, nranks)
+    ml = max(nl for _, nl in parts)
+    g = ga.LocalGroup(nranks)
+    ctxs = [ga.Context(N, m, device=0, line0=l0, nlines=nl) for l0, nl in parts]
+    for r, c in enumerate(ctxs):
+        c.comm_init_local(g, r, ml)
+    for c in ctxs:
+        c.xchg_local()
+    return g, ctxs
+
+
+def _close(g, ctxs):
+    for c in ctxs:
+        c.close()
+    g.close()
+
+
+def _check_against_single(ref, res, method):
+    assert len({(r.n_out, r.cycles_out, r.n_cycles) for r in res}) == 1
+    for r in res[1:]:
+        assert np.array_equal(res[0].hist_res, r.hist_res)
+    k = min(len(ref.hist_res), len(res[0].hist_res))
+    h, rr = res[0].hist_res[:k], ref.hist_res[:k]
+    tol = np.where(rr > 1e-6, 1e-9, 1e-3 if method == "mgsr" else 0.25)
+    assert np.all(np.abs(h - rr) <= tol * rr + 1e-16), (h, rr)
+    x = np.concatenate([r.x for r in res])
+    if ref.hist_res[-1] > 1e-6:
+        assert np.allclose(x, ref.x, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3])
+def test_selftest_in_process(nranks):
+    g, ctxs = _local_group(40, 8, nranks)
+    ok = _run_threads(nranks, lambda r: ctxs[r].xchg_selftest(5000))
+    _close(g, ctxs)
+    assert all(ok), [getattr(c, "xchg_error", "") for c in ctxs]
+
+
+def test_missing_peer_times_out_instead_of_hanging():
+    """Only rank 0 enters the exchange: its wait hits the deadline, the call
+    reports the failure (no GPU hang) and the exchange is switched off."""
+    import gmres_amd as ga
+
+    g, ctxs = _local_group(32, 4, 2)
+    assert ctxs[0].xchg_selftest(300) is False
+    assert "deadline" in ctxs[0].xchg_error
+    _close(g, ctxs)
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+@pytest.mark.parametrize("method,prec,degree", [("mgsr", "identity", 1), ("mgsr", "cbpr2", 1), ("mgsr", "cheb", 4),
+                                                ("hh", "identity", 1), ("hh", "cbpr2", 1)])
+def test_slabs_match_single_context(nranks, method, prec, degree):
+    N, m, cyc = 66, 16, 6
+    ref = _single(N, m, method, prec, degree, cyc)
+    g, ctxs = _local_group(N, m, nranks)
+
+    def work(r):
+        c = ctxs[r]
+        c.set_precond(prec, (8.2, 0.2), degree)
+        c.set_rhs_ones()
+        return _solve(c, method, prec, cyc)
+
+    res = _run_threads(nranks, work)
+    _close(g, ctxs)
+    _check_against_single(ref, res, method)
+
+
+def test_lanczos_and_verr_over_device_exchange():
+    import gmres_amd as ga
+
+    N = 40
+    with ga.Context(N, 8) as c:
+        ref = c.lanczos_bounds(30)
+    g, ctxs = _local_group(N, 12, 3)
+    out = _run_threads(3, lambda r: ctxs[r].lanczos_bounds(30))
+    assert out[0] == out[1] == out[2]
+    assert out[0][0] == pytest.approx(ref[0], rel=1e-9) and out[0][1] == pytest.approx(ref[1], rel=1e-12)
+
+    def solve(r):
+        c = ctxs[r]
+        c.set_precond("cbpr2", (8.2, 0.2), 1)
+        c.set_rhs_ones()
+        return ga.gmres_mgsr(c, 1e-15, max_cycles=1000)
+
+    res = _run_threads(3, solve)
+    _close(g, ctxs)
+    x = np.concatenate([r.x for r in res])
+    assert np.max(np.abs(x - 1.0)) < 1e-9
+    assert 0 <= res[0].v_err[res[0].n_out - 1] < 1e-12
+
+
+# ---------------------------------------------------- several processes ----
+
+def _proc_worker(rank, nranks, N, m, cyc, hq, hin, outq):
+    try:
+        import gmres_amd as ga
+
+        parts = ga.slab_partition(N, nranks)
+        ml = max(nl for _, nl in parts)
+        l0, nl = parts[rank]
+        c = ga.Context(N, m, device=0, line0=l0, nlines=nl)
+        c.comm_init_xgmi(nranks, rank, ml)
+        hq.put((rank, c.xchg_handle()))
+        handles = hin.get(timeout=120)
+        c.xchg_open(handles)
+        ok = c.xchg_selftest(10000)
+        if not ok:
+            outq.put((rank, "selftest", getattr(c, "xchg_error", "")))
+            return
+        c.set_precond("cbpr2", (8.2, 0.2), 1)
+        c.set_rhs_ones()
+        r = ga.gmres_mgsr(c, 1e-15, max_cycles=cyc, want_hist=True)
+        outq.put((rank, "ok", (r.x, r.hist_res, r.n_out, r.cycles_out, r.n_cycles)))
+        c.close()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        outq.put((rank, "error", repr(e)))
+
+
+@pytest.mark.parametrize("nranks", [2])
+def test_processes_share_regions_by_ipc(nranks):
+    """Two processes on one GPU, regions exchanged as IPC handles (the
+    multi-GPU setup path of bench.py without RCCL)."""
+    N, m, cyc = 64, 16, 4
+    ref = _single(N, m, "mgsr", "cbpr2", 1, cyc)
+    ctx = mp.get_context("spawn")
+    hq, outq = ctx.Queue(), ctx.Queue()
+    hins = [ctx.Queue() for _ in range(nranks)]
+    ps = [ctx.Process(target=_proc_worker, args=(r, nranks, N, m, cyc, hq, hins[r], outq)) for r in range(nranks)]
+    for p in ps:
+        p.start()
+    try:
+        hs = dict(hq.get(timeout=300) for _ in range(nranks))
+        for q in hins:
+            q.put([hs[r] for r in range(nranks)])
+        got = dict((r, (kind, val)) for r, kind, val in (outq.get(timeout=300) for _ in range(nranks)))
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(nranks):
+        assert got[r][0] == "ok", got[r]
+    res = [got[r][1] for r in range(nranks)]
+    assert len({(v[2], v[3], v[4]) for v in res}) == 1
+    assert all(np.array_equal(res[0][1], v[1]) for v in res)
+    x = np.concatenate([v[0] for v in res])
+    k = min(len(ref.hist_res), len(res[0][1]))
+    assert np.allclose(res[0][1][:k], ref.hist_res[:k], rtol=1e-9, atol=1e-16)
+    assert np.allclose(x, ref.x, rtol=1e-9, atol=1e-12)

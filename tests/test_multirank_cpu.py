@@ -85,3 +85,79 @@ def test_slab_protocol_matches_single_rank(oracle, world, method, prec):
         tol = np.where(r > 1e-5, 1e-8, 0.25)
     assert np.all(np.abs(h - r) <= tol * r + 1e-16)
     assert np.max(np.abs(x - 1.0)) < 1e-9
+
+
+class _FakeCtx:
+    """Stands in for gmres_amd.Context in bench.setup_xgmi (host logic only)."""
+
+    def __init__(self, rank, fail_open, fail_test):
+        self.rank, self.fail_open, self.fail_test = rank, fail_open, fail_test
+        self.enabled = None
+        self.opened = None
+
+    def xchg_handle(self):
+        return bytes([self.rank]) * 64
+
+    def xchg_open(self, hs):
+        if self.fail_open:
+            raise RuntimeError("ipc open refused")
+        self.opened = hs
+
+    def xchg_selftest(self, timeout_ms):
+        if self.fail_test:
+            self.xchg_error = "a peer missed the deadline"
+        return not self.fail_test
+
+    def xchg_enable(self, on):
+        self.enabled = on
+
+
+def _setup_worker(rank, world, port, mode, q):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    c = _FakeCtx(rank, fail_open=(mode == "open" and rank == 1), fail_test=(mode == "test" and rank == 0))
+    try:
+        out = bench.setup_xgmi(c, dist, world, rank, required=False)
+    except Exception as e:  # pragma: no cover
+        out = repr(e)
+    q.put((rank, out, c.enabled, c.opened))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["pass", "open", "test"])
+def test_bench_collective_agreement(mode):
+    """bench.py --collective auto: the device exchange is used only if every
+    rank mapped the regions and passed the self-test; otherwise every rank
+    switches it off and stays on RCCL (no rank may diverge)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_setup_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    outs = {r[1] for r in res}
+    assert len(outs) == 1
+    if mode == "pass":
+        assert outs == {"xgmi-device-exchange"}
+        assert all(r[3] == [bytes([k]) * 64 for k in range(world)] for r in res)
+    else:
+        assert outs == {None}
+        for rank, _, enabled, opened in res:
+            # ranks whose own open + self-test passed must switch the exchange off
+            own_ok = not ((mode == "open" and rank == 1) or (mode == "test" and rank == 0))
+            assert enabled is (False if own_ok else None)
