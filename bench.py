@@ -60,6 +60,13 @@ def proj_alg_bytes(n: int, steps_js: list[int]) -> float:
     return float(sum((2 * j - 1) * 40 * n + 32 * n for j in steps_js))
 
 
+def res_alg_bytes(n: int, j: int) -> float:
+    """Algorithmic bytes of one resident-step launch (step j): the reference's
+    MGS-R cascade as written, 2j x (dot 16n + AXPY 24n), + norm 8n + scale 16n
+    (SURVEY 8(d) per-step model without the 16n stencil, which is its own launch)."""
+    return float((80 * j + 24) * n)
+
+
 def cpu_baseline(N: int, m: int, prec: str, degree: int, sample_steps: int, threads: int) -> dict:
     """Reference CPU path (the oracle, a loop-for-loop restatement of
     gmres_mgsr_omp) on this host: the first `sample_steps` Arnoldi steps of
@@ -218,7 +225,36 @@ def main() -> None:
         bytes_cycle = alg_bytes_cycle(n, m, args.prec, args.degree)
         gbps_alg = bytes_cycle * cycles / elapsed / 1e9 if cycles == args.steps else None
         roof = None
-        if prof and prof["proj"][1] > 0:
+        if prof and prof.get("res", (0.0, 0))[1] > 0:
+            # resident MGS-R step: one launch = the 2j projections + norm + scale of step j
+            ms, launches = prof["res"]
+            S = max(1, args.prof_every)
+            steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
+            palg = float(sum(res_alg_bytes(nloc, j) for j in steps_js))
+            achieved = palg / (ms / 1e3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "kernel": "gk::k_mgs_res (resident MGS-R step: 2j fused projections + norm + scale, one "
+                              "persistent launch per Arnoldi step)",
+                    "launches": launches, "avg_launch_us": round(ms * 1e3 / launches, 2),
+                    "alg_bytes_per_launch": round(palg / launches),
+                    "per_projection_us": round(ms * 1e3 / sum(2 * j + 1 for j in steps_js), 2),
+                    "timing": f"HIP events on the context stream around the step launch of steps j % {S} == 0 "
+                              f"of the timed cycles",
+                    "per_kernel_ms_sampled": {k: round(v[0], 3) for k, v in prof.items()}}
+            tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            key = f"{N}_{m}_{args.prec}_{args.method}_{world}_res"
+            if os.path.exists(tf):
+                pm = json.load(open(tf))
+                if key in pm:
+                    # PMC bytes per launch are linear in the projection count: a + b (2j + 1)
+                    a0, b0 = pm[key]["bytes_fixed"], pm[key]["bytes_per_projection"]
+                    tb = sum(a0 + b0 * (2 * j + 1) for j in steps_js) / len(steps_js)
+                    roof["traffic"] = round(tb)
+                    roof["traffic_source"] = pm[key]["source"]
+                    roof["physical"] = {"fabric_GBps": round(tb * launches / (ms / 1e3) / 1e9, 1),
+                                        "bytes_per_projection": round(b0)}
+        elif prof and prof["proj"][1] > 0:
             ms, launches = prof["proj"]
             S = 1 if args.method == "hh" else max(1, args.prof_every)
             steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles

@@ -21,9 +21,10 @@ HEADER = os.path.join(os.path.dirname(PKG), "include", "gmres_hip.h")
 GK_OK = 0
 GK_ERR_COMM = -6
 GK_TUNE_XCHG_TIMEOUT_MS = 7
+GK_TUNE_RES, GK_TUNE_RES_R2, GK_TUNE_RES_SHARE, GK_TUNE_RES_TIMEOUT_MS = 8, 9, 10, 11
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
-GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER = range(6)
-KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other"]
+GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES = range(7)
+KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res"]
 
 c_int, c_double, c_ll, c_vp = ctypes.c_int, ctypes.c_double, ctypes.c_longlong, ctypes.c_void_p
 _dp = ctypes.POINTER(ctypes.c_double)

@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -125,6 +126,16 @@ struct gk_ctx {
     long long xs_tick_per_ms = 100000;
     int xs_timeout_ms = 20000;
     gk::u64 xs_timeout = 0;
+    // resident MGS-R step (gk::k_mgs_res): one persistent launch per Arnoldi step
+    gk::u64 *res_gath = nullptr;                    // [2][RGMAX][2] all-gather granules
+    int *res_err = nullptr, *res_err_dev = nullptr;  // mapped deadline flag
+    unsigned res_tag = 1;                           // next granule tag (never 0)
+    int res_cus = 0;                                // compute units of the device
+    int tune_res = -1;                              // -1 auto, 0 off, 1 on where possible
+    int tune_res_r2 = 0;                            // cap of resident double2 per thread (0 = auto)
+    int res_share = 1;                              // contexts sharing this device's CUs
+    int res_timeout_ms = 20000;
+    bool res_broken = false;                        // a deadline was missed: launch path from then on
     // launch geometry
     int vec = 2, JT = 16;
     dim3 sgrid;
@@ -232,8 +243,23 @@ int xs_check(gk_ctx *c) {
     return GK_OK;
 }
 
+// After a host wait: did a resident step miss an in-launch deadline?  Then the
+// context falls back to one launch per projection for the rest of its life.
+int res_check(gk_ctx *c) {
+    if (c->res_err != nullptr && __atomic_load_n(c->res_err, __ATOMIC_ACQUIRE) != 0) {
+        *c->res_err = 0;
+        c->res_broken = true;
+        return set_err(GK_ERR_COMM,
+                       "resident MGS-R step: an in-launch exchange missed its %d ms deadline (workgroups not "
+                       "co-resident?); the launch-per-projection path is used from now on",
+                       c->res_timeout_ms);
+    }
+    return GK_OK;
+}
+
 int sync_st(gk_ctx *c) {
     HIPCHK(hipStreamSynchronize(c->st));
+    CHK(res_check(c));
     return xs_check(c);
 }
 
@@ -534,6 +560,104 @@ int finalize(gk_ctx *c, const double *pin, int npin, double *out, int take_sqrt)
     gk::k_finalize<<<1, gk::TPB, 0, c->st>>>(pin, npin, out, take_sqrt);
     LAUNCHCHK();
     return GK_OK;
+}
+
+// ------------------------------------------------ resident MGS-R step ----
+constexpr int RES_LDS = 96 * 1024;  // dynamic LDS: > half a CU's 160 KiB, so one workgroup per CU
+
+struct ResPlan {
+    int G = 0, r2 = 0;
+    bool pf = false, nt = false;
+    i64 nres2 = 0;
+};
+
+// Can step j run as one resident launch, and with which variant?  Needs an
+// in-launch reduction path: single rank, or the device exchange (RCCL and the
+// host-side local group cannot be driven from inside a kernel).
+bool res_plan(gk_ctx *c, ResPlan &p) {
+    if (c->tune_res == 0 || c->res_broken || c->m > gk::RHMAX || c->res_cus <= 0 || c->res_gath == nullptr)
+        return false;
+    if (collective(c) && !(c->xs_on && c->nranks > 1)) return false;
+    // Several resident launches on one device spin on each other's partials, so
+    // their streams must run concurrently -- HIP promises nothing about how
+    // streams map to hardware queues.  Auto mode assumes one context per device.
+    if (c->tune_res < 0 && c->res_share > 1) return false;
+    p.G = std::max(1, std::min(gk::RGMAX, c->res_cus / std::max(1, c->res_share)));
+    const i64 n2 = c->nloc / 2, per_r2 = (i64)p.G * gk::RT;
+    const i64 need = (n2 + per_r2 - 1) / per_r2;  // double2 per thread to hold the whole vector
+    const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : 16;
+    static const int sizes[] = {2, 4, 8, 16};
+    p.r2 = 0;
+    for (int s : sizes)
+        if (s <= cap && (p.r2 == 0 || p.r2 < need)) p.r2 = s;
+    p.pf = p.r2 <= 8;  // three register arrays fit; 16 keeps two (w, the running column)
+    p.nres2 = std::min<i64>(n2 / gk::RT * gk::RT, per_r2 * p.r2);  // whole chunks of RT double2
+    p.nt = c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto);
+    return true;
+}
+
+template <int R2, bool PF, bool NT>
+int launch_res_t(gk_ctx *c, int G, const gk::ResArgs &a) {
+    static std::atomic<bool> attr{false};
+    if (!attr.load()) {
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_res<R2, PF, NT>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS));
+        attr = true;
+    }
+    gk::k_mgs_res<R2, PF, NT><<<G, gk::RT, RES_LDS, c->st>>>(a);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
+int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+#define GK_RES_CASE(R, PFV)                                                                             \
+    if (p.r2 == R && p.pf == PFV)                                                                       \
+        return p.nt ? launch_res_t<R, PFV, true>(c, p.G, a) : launch_res_t<R, PFV, false>(c, p.G, a);
+    GK_RES_CASE(2, true)
+    GK_RES_CASE(4, true)
+    GK_RES_CASE(8, true)
+    GK_RES_CASE(16, false)
+#undef GK_RES_CASE
+    return set_err(GK_ERR_ARG, "no resident variant for r2=%d", p.r2);
+}
+
+// The MGS cascade of step j + norm + scale as one launch; pin/npin = the
+// (all-reduced) partial slab of the first dot <w, V(:,1)>.
+int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, double *hs, double *hcopy) {
+    ProfScope ps(c, GK_KID_RES);
+    const int np = 2 * j;
+    if (c->res_tag > 0xF0000000u) {  // tags must never repeat within the granule region's lifetime
+        HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * 4 * gk::RGMAX, c->st));
+        c->res_tag = 1;
+    }
+    gk::ResArgs a{};
+    a.w = c->w;
+    a.V = c->V;
+    a.vout = c->V + (i64)j * c->ld;
+    a.ld = c->ld;
+    a.pin = pin;
+    a.npin = npin;
+    a.hs = hs;
+    a.hcopy = hcopy;
+    a.gath = c->res_gath;
+    a.j = j;
+    a.n = c->nloc;
+    a.nres2 = p.nres2;
+    a.tag0 = c->res_tag;
+    c->res_tag += (unsigned)np;
+    a.timeout = (gk::u64)c->res_timeout_ms * (gk::u64)c->xs_tick_per_ms;
+    a.err = c->res_err_dev;
+    a.nranks = 1;
+    if (c->xs_on && c->nranks > 1) {
+        a.err = c->xs_err_dev;
+        a.timeout = std::max(a.timeout, c->xs_timeout);
+        a.peers = c->xs_peers;
+        a.nranks = c->nranks;
+        a.rank = c->rank;
+        a.xseq0 = c->xs_seq;
+        c->xs_seq += (unsigned)np;
+    }
+    return launch_res(c, p, a);
 }
 
 int d2h_sync(gk_ctx *c, double *host, const double *dev, int count) {
@@ -846,6 +970,18 @@ int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out)
         hipHostMalloc(&c->hallh, sizeof(double) * (size_t)(m + 2) * (m + 1), hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void **)&c->hallh_dev, c->hallh, 0) != hipSuccess)
         return fail(set_err(GK_ERR_NOMEM, "cannot allocate the Hessenberg mirrors"));
+    if (hipMalloc(&c->res_gath, sizeof(gk::u64) * 4 * gk::RGMAX) != hipSuccess ||
+        hipHostMalloc((void **)&c->res_err, sizeof(int), hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->res_err_dev, c->res_err, 0) != hipSuccess ||
+        hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * 4 * gk::RGMAX, c->st) != hipSuccess)
+        return fail(set_err(GK_ERR_NOMEM, "cannot allocate the resident-step exchange area"));
+    *c->res_err = 0;
+    {
+        int cus = 0, khz = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) c->res_cus = cus;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+            c->xs_tick_per_ms = khz;
+    }
     c->ev_step.assign(m + 1, nullptr);
     for (int k = 0; k <= m; ++k)
         if (hipEventCreateWithFlags(&c->ev_step[k], hipEventDisableTiming) != hipSuccess)
@@ -877,6 +1013,8 @@ int gk_destroy(gk_ctx *c) {
     for (void *p : c->xs_mapped) (void)hipIpcCloseMemHandle(p);
     if (c->xs_buf) (void)hipFree(c->xs_buf);
     if (c->xs_err) (void)hipHostFree(c->xs_err);
+    if (c->res_gath) (void)hipFree(c->res_gath);
+    if (c->res_err) (void)hipHostFree(c->res_err);
     double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi,
                       c->red, c->hcol, c->ydev, c->hb, c->scal, c->Vb, c->gram_slab, c->gram_out};
     for (double *p : bufs)
@@ -948,6 +1086,7 @@ int gk_comm_init_local(gk_ctx *c, gk_group *g, int rank, int max_lines) {
     c->max_lines = max_lines;
     set_geometry(c);
     c->lg = g;
+    c->res_share = g->n;  // members may share one device: resident launches split its CUs
     HIPCHK(hipEventCreateWithFlags(&c->lev_a, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->lev_b, hipEventDisableTiming));
     if (hipMalloc(&c->lscratch, sizeof(double) * gk::NPMAX * 4) != hipSuccess)
@@ -1242,6 +1381,14 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
     // w = M^-1 A V(:,j), fused with the first dot <w, V(:,1)>
     CHK(op_precond(c, V + (i64)(j - 1) * ld, c->w, false, gk::ACC_DOT, V, slot(c, s0)));
     int np = c->last_np;
+    ResPlan rp;
+    if (res_plan(c, rp)) {  // the whole cascade + norm + scale as one resident launch
+        CHK(allreduce(c, slot(c, s0), np));
+        CHK(res_step(c, j, rp, slot(c, s0), np, hs, c->hallh_dev + (i64)(j - 1) * m2));
+        HIPCHK(hipEventRecord(c->ev_step[j], c->st));
+        c->prof_on_step = true;
+        return GK_OK;
+    }
     // two MGS passes: projection p = (k, i), AXPY of p fused with the dot of p+1
     const int np_total = 2 * j;
     for (int p = 0; p < np_total; ++p) {
@@ -1271,6 +1418,7 @@ int gk_mgs_step_wait(gk_ctx *c, int j, double *hcol) {
     CHK(check_ctx(c));
     if (j < 1 || j > c->m) return set_err(GK_ERR_ARG, "step j=%d outside 1..%d", j, c->m);
     HIPCHK(hipEventSynchronize(c->ev_step[j]));
+    CHK(res_check(c));
     CHK(xs_check(c));
     const volatile double *src = c->hallh + (i64)(j - 1) * (c->m + 2);
     for (int k = 0; k <= j; ++k) hcol[k] = src[k];
@@ -1525,6 +1673,20 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_XCHG_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
             xs_set_timeout(c, value);
+            break;
+        case GK_TUNE_RES: c->tune_res = value < 0 ? -1 : (value != 0); break;
+        case GK_TUNE_RES_R2:
+            if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16)
+                return set_err(GK_ERR_ARG, "resident cap must be 0 (auto), 2, 4, 8 or 16");
+            c->tune_res_r2 = value;
+            break;
+        case GK_TUNE_RES_SHARE:
+            if (value < 1) return set_err(GK_ERR_ARG, "share must be >= 1");
+            c->res_share = value;
+            break;
+        case GK_TUNE_RES_TIMEOUT_MS:
+            if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
+            c->res_timeout_ms = value;
             break;
         case GK_TUNE_PROJ_UNROLL:
             if (value != 0 && value != 2 && value != 4 && value != 8)

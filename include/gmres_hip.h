@@ -52,7 +52,8 @@ extern "C" {
 #define GK_KID_UPDATE 3  /* x += V y */
 #define GK_KID_COMM 4    /* all-reduce / halo / broadcast (RCCL or device exchange) */
 #define GK_KID_OTHER 5
-#define GK_NKID 6
+#define GK_KID_RES 6     /* resident MGS-R step: whole cascade + norm + scale in one launch */
+#define GK_NKID 7
 
 typedef struct gk_ctx gk_ctx;
 typedef struct gk_group gk_group;
@@ -216,7 +217,18 @@ int gk_sync(gk_ctx *ctx);
  *   GK_TUNE_PROJ_UNROLL    double2 loads in flight per thread and array: 2, 4, 8; 0 = auto
  *   GK_TUNE_CHEB_FUSED     1 (default): Chebyshev(k <= 8) as temporal-blocked passes of up to
  *                          4 sweeps each (single slab, even N); 0: one launch per sweep
- *   GK_TUNE_XCHG_TIMEOUT_MS deadline of one device-exchange wait (default 20000) */
+ *   GK_TUNE_XCHG_TIMEOUT_MS deadline of one device-exchange wait (default 20000)
+ *   GK_TUNE_RES            resident MGS-R step (one persistent launch per Arnoldi step, w and the
+ *                          running Krylov column held in registers, dots all-gathered inside the
+ *                          launch): -1 auto (default: on for a single rank or the device exchange,
+ *                          m <= 512, one context per device), 1 also with several contexts on one
+ *                          device (their streams must then run concurrently), 0 off (one launch
+ *                          per projection)
+ *   GK_TUNE_RES_R2         cap of register-resident double2 per thread and array: 0 auto, 2/4/8/16
+ *   GK_TUNE_RES_SHARE      contexts sharing this device (resident launches use CUs / share
+ *                          workgroups; gk_comm_init_local sets it to the group size)
+ *   GK_TUNE_RES_TIMEOUT_MS deadline of one in-launch wait (default 20000); a miss fails the step
+ *                          with GK_ERR_COMM and switches the context to the launch path */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
@@ -225,6 +237,10 @@ int gk_sync(gk_ctx *ctx);
 #define GK_TUNE_PROJ_UNROLL 5
 #define GK_TUNE_CHEB_FUSED 6
 #define GK_TUNE_XCHG_TIMEOUT_MS 7
+#define GK_TUNE_RES 8
+#define GK_TUNE_RES_R2 9
+#define GK_TUNE_RES_SHARE 10
+#define GK_TUNE_RES_TIMEOUT_MS 11
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

@@ -1,0 +1,95 @@
+"""Resident MGS-R step (gk::k_mgs_res, include/gmres_hip.h GK_TUNE_RES): the whole
+cascade of an Arnoldi step (gmres_mgsr.f90:341-363, :384) in ONE persistent launch,
+w and the running Krylov column held in registers, the dots all-gathered inside the
+launch.
+
+Parity: the element-wise arithmetic is the launch path's (k_proj / k_scale), only the
+dot summation order differs, so the per-cycle true residuals must agree with the
+launch-per-projection path to reduction-order noise and with the CPU oracle within the
+reference's own tolerance.  The variants cover: fully resident with the
+next column prefetched (R2 2/4/8), two-array residency (R2 16), a partly streamed
+vector (cap below the vector size, few workgroups), odd N (tail element), every
+preconditioner.  Determinism: two runs give bit-identical histories.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+T_RES, T_R2, T_SHARE, T_TMO = 8, 9, 10, 11
+
+
+def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False):
+    import gmres_amd as ga
+
+    with ga.Context(N, m) as c:
+        c.tune(T_RES, res)
+        c.tune(T_R2, r2)
+        c.tune(T_SHARE, share)
+        c.tune(T_TMO, 5000)
+        c.set_precond(prec, (8.2, 0.2), degree)
+        c.set_rhs_ones()
+        if want_prof:
+            c.profile(True)
+            c.profile_reset()
+        r = ga.gmres_mgsr(c, 1e-15, max_cycles=cycles, want_hist=True)
+        prof = c.profile_read() if want_prof else None
+    return r, prof
+
+
+CASES = [
+    # N, m, prec, r2 cap, share (workgroups = CUs / share)
+    (64, 20, "identity", 0, 1),      # fully resident, R2 = 2, prefetch
+    (130, 30, "cbpr2", 2, 8),        # 32 workgroups x 512 x 2 < n/2: streamed tail of the vector
+    (45, 12, "identity", 2, 64),     # odd N: the tail element, 4 workgroups
+    (256, 40, "cheb", 16, 16),       # two-array variant
+    (200, 25, "identity", 4, 32),    # R2 = 4 with a streamed part
+    (512, 30, "identity", 8, 4),     # R2 = 8, fully resident
+]
+
+
+@pytest.mark.parametrize("N,m,prec,r2,share", CASES)
+def test_resident_matches_launch_path(N, m, prec, r2, share):
+    ref, _ = _run(N, m, prec, res=0)
+    got, prof = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True)
+    # the resident kernel ran every step (k_proj only in the off-cycle diagnostics)
+    assert prof["res"][1] > 0 and prof["proj"][1] < prof["res"][1] // 4, prof
+    assert got.n_cycles == ref.n_cycles
+    h, r = got.hist_res, ref.hist_res
+    tol = np.where(r > 1e-8, 1e-10, 1e-4)
+    assert np.all(np.abs(h - r) <= tol * r + 1e-16), (h, r)
+    k = min(got.n_out, ref.n_out)
+    assert np.allclose(got.final_err[:k], ref.final_err[:k], rtol=1e-6, atol=1e-16)
+
+
+@pytest.mark.parametrize("N,m,prec", [(128, 30, "identity"), (128, 30, "cbpr2")])
+def test_resident_vs_oracle_to_convergence(oracle, N, m, prec):
+    """Config 1 shape to tol 1e-15 on the resident path, against the oracle
+    (reference restatement) with the reference-derived tolerance."""
+    got, _ = _run(N, m, prec, res=1, cycles=1000)
+    kind = {"identity": oracle.PREC_IDENTITY, "cbpr2": oracle.PREC_CBPR2}[prec]
+    ref = oracle.gmres_mgsr(oracle.rhs_ones(N), N, m, prec=kind, variant=oracle.MGSR_OMP)
+    assert abs(got.iterations - ref.iterations) <= max(1, 0.01 * ref.iterations)
+    k = min(len(got.hist_res), len(ref.hist_res))
+    dev = np.abs(got.hist_res[:k] - ref.hist_res[:k])
+    assert np.all(dev <= 1e-5 * ref.hist_res[:k] + 1e-13)
+    assert np.max(np.abs(got.x - 1.0)) < 1e-9
+
+
+def test_resident_is_deterministic():
+    a, _ = _run(96, 24, "cbpr2", res=1, r2=2, share=16, cycles=3)
+    b, _ = _run(96, 24, "cbpr2", res=1, r2=2, share=16, cycles=3)
+    assert np.array_equal(a.hist_res, b.hist_res)
+    assert np.array_equal(a.x, b.x)
+
+
+def test_resident_1024_vs_reference():
+    """Config 2 size: the reference's own per-cycle true residuals (serial run)."""
+    import json
+    import os
+
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_known_answers.json")))
+    g = gold["mgsr_identity_1024_m95"]["cycle_true_residual"]
+    got, prof = _run(1024, 95, "identity", res=1, cycles=3, want_prof=True)
+    assert prof["res"][1] > 0
+    assert np.allclose(got.hist_res, g[: len(got.hist_res)], rtol=1e-9, atol=0.0)

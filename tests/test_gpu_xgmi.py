@@ -128,6 +128,34 @@ def test_slabs_match_single_context(nranks, method, prec, degree):
     _check_against_single(ref, res, method)
 
 
+@pytest.mark.parametrize("prec,degree", [("identity", 1), ("cbpr2", 1), ("cheb", 4)])
+def test_resident_step_over_device_exchange(prec, degree):
+    """Resident MGS-R step (one persistent launch per Arnoldi step) with the rank
+    totals exchanged inside the launch: two ranks on one GPU, forced on
+    (GK_TUNE_RES = 1; auto mode keeps it off when contexts share a device)."""
+    N, m, cyc = 66, 16, 6
+    ref = _single(N, m, "mgsr", prec, degree, cyc)
+    g, ctxs = _local_group(N, m, 2)
+    for c in ctxs:
+        c.tune(8, 1)
+        c.tune(11, 5000)
+
+    def work(r):
+        c = ctxs[r]
+        c.set_precond(prec, (8.2, 0.2), degree)
+        c.set_rhs_ones()
+        c.profile(True)
+        c.profile_reset()
+        out = _solve(c, "mgsr", prec, cyc)
+        return out, c.profile_read()
+
+    out = _run_threads(2, work)
+    _close(g, ctxs)
+    res = [o[0] for o in out]
+    assert all(o[1]["res"][1] > 0 for o in out)
+    _check_against_single(ref, res, "mgsr")
+
+
 def test_lanczos_and_verr_over_device_exchange():
     import gmres_amd as ga
 
@@ -154,7 +182,7 @@ def test_lanczos_and_verr_over_device_exchange():
 
 # ---------------------------------------------------- several processes ----
 
-def _proc_worker(rank, nranks, N, m, cyc, hq, hin, outq):
+def _proc_worker(rank, nranks, N, m, cyc, hq, hin, outq, force_res=0):
     try:
         import gmres_amd as ga
 
@@ -164,8 +192,12 @@ def _proc_worker(rank, nranks, N, m, cyc, hq, hin, outq):
         c = ga.Context(N, m, device=0, line0=l0, nlines=nl)
         c.comm_init_xgmi(nranks, rank, ml)
         hq.put((rank, c.xchg_handle()))
-        handles = hin.get(timeout=120)
+        handles = hin.get(timeout=100)
         c.xchg_open(handles)
+        c.tune(10, nranks)  # GK_TUNE_RES_SHARE: the ranks' resident launches share this one GPU
+        if force_res:
+            c.tune(8, 1)
+            c.tune(11, 5000)
         ok = c.xchg_selftest(10000)
         if not ok:
             outq.put((rank, "selftest", getattr(c, "xchg_error", "")))
@@ -179,8 +211,8 @@ def _proc_worker(rank, nranks, N, m, cyc, hq, hin, outq):
         outq.put((rank, "error", repr(e)))
 
 
-@pytest.mark.parametrize("nranks", [2])
-def test_processes_share_regions_by_ipc(nranks):
+@pytest.mark.parametrize("nranks,force_res", [(2, 0), (2, 1)])
+def test_processes_share_regions_by_ipc(nranks, force_res):
     """Two processes on one GPU, regions exchanged as IPC handles (the
     multi-GPU setup path of bench.py without RCCL)."""
     N, m, cyc = 64, 16, 4
@@ -188,14 +220,14 @@ def test_processes_share_regions_by_ipc(nranks):
     ctx = mp.get_context("spawn")
     hq, outq = ctx.Queue(), ctx.Queue()
     hins = [ctx.Queue() for _ in range(nranks)]
-    ps = [ctx.Process(target=_proc_worker, args=(r, nranks, N, m, cyc, hq, hins[r], outq)) for r in range(nranks)]
+    ps = [ctx.Process(target=_proc_worker, args=(r, nranks, N, m, cyc, hq, hins[r], outq, force_res)) for r in range(nranks)]
     for p in ps:
         p.start()
     try:
-        hs = dict(hq.get(timeout=300) for _ in range(nranks))
+        hs = dict(hq.get(timeout=100) for _ in range(nranks))
         for q in hins:
             q.put([hs[r] for r in range(nranks)])
-        got = dict((r, (kind, val)) for r, kind, val in (outq.get(timeout=300) for _ in range(nranks)))
+        got = dict((r, (kind, val)) for r, kind, val in (outq.get(timeout=100) for _ in range(nranks)))
     finally:
         for p in ps:
             p.join(timeout=60)

@@ -16,8 +16,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KEYS = {"nt": 0, "pj": 1, "st": 2, "rev": 3, "blk": 4, "unr": 5, "cf": 6}
-DEFAULTS = {0: -1, 1: 0, 2: 0, 3: 0, 4: 0, 5: 0, 6: 1}
+KEYS = {"nt": 0, "pj": 1, "st": 2, "rev": 3, "blk": 4, "unr": 5, "cf": 6, "res": 8, "rr2": 9}
+DEFAULTS = {0: -1, 1: 0, 2: 0, 3: 0, 4: 0, 5: 0, 6: 1, 8: -1, 9: 0}
 
 
 def parse_variant(s: str) -> dict:
@@ -64,7 +64,7 @@ def main():
             ga.gmres_mgsr(ctx, 1e-15, max_cycles=1, want_verr=False)
             p = ctx.profile_read()
             ctx.profile(False)
-            res[v]["proj_us"].append(p["proj"][0] * 1e3 / max(p["proj"][1], 1))
+            res[v]["proj_us"].append(p["proj"][0] * 1e3 / max(p["proj"][1], 1) if p["proj"][1] else p["res"][0] * 1e3 / max(p["res"][1], 1))
             res[v]["breakdown_ms"] = {k: round(x[0], 3) for k, x in p.items()}
             print(json.dumps({"round": r, "variant": v, "wall_ms": round(res[v]["wall_ms"][-1], 2),
                               "proj_us": round(res[v]["proj_us"][-1], 2), "resid": res[v]["resid"]}), flush=True)
