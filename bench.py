@@ -198,8 +198,29 @@ def main() -> None:
         if dist is not None:
             dist.barrier()
 
-    if args.warmup > 0:
-        run(args.warmup)
+    def guarded_warmup() -> bool:
+        ok = 1
+        try:
+            if args.warmup > 0:
+                run(args.warmup)
+        except Exception as e:  # noqa: BLE001 - every rank reports, then all agree below
+            print(f"rank {rank}: warmup failed: {e}", file=sys.stderr)
+            ok = 0
+        if dist is not None:
+            t = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = int(t.item())
+        return ok == 1
+
+    if not guarded_warmup():
+        # Fallback, decided by all ranks together: the launch-per-projection path
+        # (and RCCL instead of the device exchange when that was in use).
+        if collective == "xgmi-device-exchange" and args.collective == "auto":
+            ctx.xchg_enable(False)
+            collective = "rccl (device exchange failed in warmup)"
+        ctx.tune(8, 0)  # GK_TUNE_RES off
+        if not guarded_warmup():
+            raise RuntimeError("warmup failed on the fallback path too")
     if not args.no_prof:
         ctx.profile(1 if args.method == "hh" else max(1, args.prof_every))
         ctx.profile_reset()
@@ -247,9 +268,9 @@ def main() -> None:
             if os.path.exists(tf):
                 pm = json.load(open(tf))
                 if key in pm:
-                    # PMC bytes per launch are linear in the projection count: a + b (2j + 1)
+                    # PMC bytes per launch are linear in the projection count: a + b 2j
                     a0, b0 = pm[key]["bytes_fixed"], pm[key]["bytes_per_projection"]
-                    tb = sum(a0 + b0 * (2 * j + 1) for j in steps_js) / len(steps_js)
+                    tb = sum(a0 + b0 * 2 * j for j in steps_js) / len(steps_js)
                     roof["traffic"] = round(tb)
                     roof["traffic_source"] = pm[key]["source"]
                     roof["physical"] = {"fabric_GBps": round(tb * launches / (ms / 1e3) / 1e9, 1),

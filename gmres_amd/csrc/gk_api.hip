@@ -1166,6 +1166,7 @@ int gk_xchg_enable(gk_ctx *c, int on) {
     if (!on && c->comm == nullptr && c->lg == nullptr && c->nranks > 1)
         return set_err(GK_ERR_STATE, "no RCCL or local communicator to fall back to");
     c->xs_on = on != 0;
+    if (!c->xs_on && c->xs_err != nullptr) *c->xs_err = 0;  // a missed deadline does not outlive the switch
     return GK_OK;
 }
 

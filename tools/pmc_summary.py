@@ -24,6 +24,36 @@ def per_launch(path, kernel):
     return statistics.median(vals) * 1024.0, len(vals)  # counters are in KB
 
 
+def series(path, kernel):
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    return [float(r["Counter_Value"]) * 1024.0 for r in rows]
+
+
+def res_fit(a):
+    """Least-squares fit of the per-launch bytes of the resident step kernel
+    against its projection count 2j (j = 1..probe_m, launch order)."""
+    import numpy as np
+
+    f = np.array(series(a.fetch, a.kernel)) * 2.0  # gfx950 FETCH_SIZE correction
+    w = np.array(series(a.write, a.kernel))
+    k = min(len(f), len(w))
+    x = np.array([2 * (i % a.probe_m + 1) for i in range(k)], dtype=float)
+    y = f[:k] + w[:k]
+    b, c = np.polyfit(x, y, 1)
+    n = a.grid * a.grid // a.gpus
+    entry = {"kernel": a.kernel, "launches_sampled": k, "bytes_fixed": float(c), "bytes_per_projection": float(b),
+             "bytes_per_unknown_per_projection": float(b) / n,
+             "fit_residual_max_rel": float(np.max(np.abs(y - (b * x + c)) / y)),
+             "source": f"{os.path.relpath(a.fetch)} + {os.path.relpath(a.write)} (per launch j = 1..{a.probe_m}, "
+                       "FETCH_SIZE x2 gfx950 correction, linear fit in the projection count 2j; L2<->fabric "
+                       "bytes incl. Infinity-Cache hits)"}
+    db = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    db[f"{a.grid}_{a.m}_{a.prec}_{a.method}_{a.gpus}_res"] = entry
+    json.dump(db, open(a.out, "w"), indent=1)
+    print(json.dumps(entry, indent=1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
@@ -34,9 +64,15 @@ def main():
     ap.add_argument("--method", default="mgsr")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--kernel", default="gk::k_proj<2")
+    ap.add_argument("--res", action="store_true",
+                    help="resident-step kernel (one launch per Arnoldi step j = 1..probe-m in launch order): "
+                         "fit bytes per launch = fixed + per_projection * 2j")
+    ap.add_argument("--probe-m", type=int, default=8)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
+    if a.res:
+        return res_fit(a)
     f, nf = per_launch(a.fetch, a.kernel)
     w, nw = per_launch(a.write, a.kernel)
     n = a.grid * a.grid // a.gpus
