@@ -133,6 +133,7 @@ struct gk_ctx {
     int res_cus = 0;                                // compute units of the device
     int tune_res = -1;                              // -1 auto, 0 off, 1 on where possible
     int tune_res_r2 = 0;                            // cap of resident double2 per thread (0 = auto)
+    int tune_res_lds = 1;                           // LDS-resident part of w for large slabs
     int res_share = 1;                              // contexts sharing this device's CUs
     int res_timeout_ms = 20000;
     bool res_broken = false;                        // a deadline was missed: launch path from then on
@@ -563,17 +564,24 @@ int finalize(gk_ctx *c, const double *pin, int npin, double *out, int take_sqrt)
 }
 
 // ------------------------------------------------ resident MGS-R step ----
-constexpr int RES_LDS = 96 * 1024;  // dynamic LDS: > half a CU's 160 KiB, so one workgroup per CU
+constexpr int RES_LDS_MIN = 96 * 1024;  // dynamic LDS: > half a CU's 160 KiB, so one workgroup per CU
+constexpr int RES_L2 = 18;              // LDS-resident double2 of w per data thread (18 x 512 x 16 B = 144 KiB)
+constexpr int RES_R2_BIG = 12;          // two register arrays of 12 double2 fit 256 VGPRs without spills
 
 struct ResPlan {
-    int G = 0, r2 = 0;
-    bool pf = false, nt = false;
+    int G = 0, r2 = 0, l2 = 0;
+    bool pf = false, nt = false, cw = false;
     i64 nres2 = 0;
+    int lds = 0;
 };
 
 // Can step j run as one resident launch, and with which variant?  Needs an
 // in-launch reduction path: single rank, or the device exchange (RCCL and the
 // host-side local group cannot be driven from inside a kernel).
+//   fits in 3 x R2 <= 8 registers (w, running column, prefetched column) with
+//   wave 0 kept for the exchange: R2 in {2,4,8}, PF + CW;
+//   else w and the running column in 2 x 12 registers, plus (GK_TUNE_RES_LDS)
+//   w of 18 more chunks per workgroup in LDS, the rest streamed.
 bool res_plan(gk_ctx *c, ResPlan &p) {
     if (c->tune_res == 0 || c->res_broken || c->m > gk::RHMAX || c->res_cus <= 0 || c->res_gath == nullptr)
         return false;
@@ -582,43 +590,57 @@ bool res_plan(gk_ctx *c, ResPlan &p) {
     // their streams must run concurrently -- HIP promises nothing about how
     // streams map to hardware queues.  Auto mode assumes one context per device.
     if (c->tune_res < 0 && c->res_share > 1) return false;
-    p.G = std::max(1, std::min(gk::RGMAX, c->res_cus / std::max(1, c->res_share)));
-    const i64 n2 = c->nloc / 2, per_r2 = (i64)p.G * gk::RT;
-    const i64 need = (n2 + per_r2 - 1) / per_r2;  // double2 per thread to hold the whole vector
-    const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : 16;
-    static const int sizes[] = {2, 4, 8, 16};
-    p.r2 = 0;
-    for (int s : sizes)
+    const int gmax = std::max(1, std::min(gk::RGMAX, c->res_cus / std::max(1, c->res_share)));
+    const i64 n2 = c->nloc / 2;
+    const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : RES_R2_BIG;
+    const i64 dcw = gk::RT - 64;
+    // small vectors: no more workgroups than two chunks each (a cheaper all-gather)
+    const int gcw = (int)std::max<i64>(1, std::min<i64>(gmax, (n2 + 2 * dcw - 1) / (2 * dcw)));
+    const i64 need = (n2 + (i64)gcw * dcw - 1) / ((i64)gcw * dcw);
+    p = ResPlan{};
+    static const int pfs[] = {2, 4, 8};
+    for (int s : pfs)
         if (s <= cap && (p.r2 == 0 || p.r2 < need)) p.r2 = s;
-    p.pf = p.r2 <= 8;  // three register arrays fit; 16 keeps two (w, the running column)
-    p.nres2 = std::min<i64>(n2 / gk::RT * gk::RT, per_r2 * p.r2);  // whole chunks of RT double2
+    if (p.r2 >= need || cap < RES_R2_BIG) {
+        p.G = gcw;
+        p.pf = p.cw = true;
+        p.nres2 = std::min<i64>(n2 / dcw * dcw, (i64)p.G * p.r2 * dcw);
+    } else {
+        p.G = gmax;
+        p.r2 = RES_R2_BIG;
+        const i64 dt = gk::RT, regs = (i64)p.G * RES_R2_BIG * dt;
+        p.l2 = (c->tune_res_lds && n2 / dt * dt > regs) ? RES_L2 : 0;
+        p.nres2 = std::min<i64>(n2 / dt * dt, (i64)p.G * (RES_R2_BIG + p.l2) * dt);
+    }
+    p.lds = std::max<int>(RES_LDS_MIN, p.l2 * (p.cw ? gk::RT - 64 : gk::RT) * (int)sizeof(double2));
     p.nt = c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto);
     return true;
 }
 
-template <int R2, bool PF, bool NT>
-int launch_res_t(gk_ctx *c, int G, const gk::ResArgs &a) {
-    static std::atomic<bool> attr{false};
-    if (!attr.load()) {
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_res<R2, PF, NT>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS));
-        attr = true;
+template <int R2, int L2, bool PF, bool NT, bool CW>
+int launch_res_t(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    static std::atomic<int> attr{0};
+    if (attr.load() < p.lds) {
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_res<R2, L2, PF, NT, CW>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
+        attr = p.lds;
     }
-    gk::k_mgs_res<R2, PF, NT><<<G, gk::RT, RES_LDS, c->st>>>(a);
+    gk::k_mgs_res<R2, L2, PF, NT, CW><<<p.G, gk::RT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
 }
 
 int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
-#define GK_RES_CASE(R, PFV)                                                                             \
-    if (p.r2 == R && p.pf == PFV)                                                                       \
-        return p.nt ? launch_res_t<R, PFV, true>(c, p.G, a) : launch_res_t<R, PFV, false>(c, p.G, a);
-    GK_RES_CASE(2, true)
-    GK_RES_CASE(4, true)
-    GK_RES_CASE(8, true)
-    GK_RES_CASE(16, false)
+#define GK_RES_CASE(R, L, PFV, CWV)                                                                 \
+    if (p.r2 == R && p.l2 == L && p.pf == PFV && p.cw == CWV)                                      \
+        return p.nt ? launch_res_t<R, L, PFV, true, CWV>(c, p, a) : launch_res_t<R, L, PFV, false, CWV>(c, p, a);
+    GK_RES_CASE(2, 0, true, true)
+    GK_RES_CASE(4, 0, true, true)
+    GK_RES_CASE(8, 0, true, true)
+    GK_RES_CASE(RES_R2_BIG, 0, false, false)
+    GK_RES_CASE(RES_R2_BIG, RES_L2, false, false)
 #undef GK_RES_CASE
-    return set_err(GK_ERR_ARG, "no resident variant for r2=%d", p.r2);
+    return set_err(GK_ERR_ARG, "no resident variant for r2=%d l2=%d", p.r2, p.l2);
 }
 
 // The MGS cascade of step j + norm + scale as one launch; pin/npin = the
@@ -1677,14 +1699,15 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
             break;
         case GK_TUNE_RES: c->tune_res = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_RES_R2:
-            if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16)
-                return set_err(GK_ERR_ARG, "resident cap must be 0 (auto), 2, 4, 8 or 16");
+            if (value != 0 && value != 2 && value != 4 && value != 8 && value != 12)
+                return set_err(GK_ERR_ARG, "resident cap must be 0 (auto), 2, 4, 8 or 12");
             c->tune_res_r2 = value;
             break;
         case GK_TUNE_RES_SHARE:
             if (value < 1) return set_err(GK_ERR_ARG, "share must be >= 1");
             c->res_share = value;
             break;
+        case GK_TUNE_RES_LDS: c->tune_res_lds = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
             c->res_timeout_ms = value;

@@ -970,126 +970,140 @@ __device__ __forceinline__ double block_sum_rt(double v, double *sm) {
     double r = sm[0];
 #pragma unroll
     for (int k = 1; k < RWAVES; ++k) r += sm[k];
+    __syncthreads();  // sm is rewritten next
     return r;
 }
 
-// Publish this workgroup's partial s of exchange p; every thread gets the
-// fixed-order total over the grid (and over ranks).  false: a deadline passed.
-__device__ __forceinline__ bool res_allreduce(const ResArgs &a, int p, double s, double &tot, double *bc,
-                                              int *okf) {
+// Wave 0 of every workgroup: sum the workgroup's wave partials sm[0..RWAVES)
+// in order, publish that sum of exchange p as two tagged granules, sweep the
+// G partials of the grid (8 granules in flight per lane) and sum them in a
+// fixed order; on N ranks then add the rank totals in rank order.  Result in
+// bc[0]; *okf = 0 when a deadline passed (then *err is set).
+__device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const double *sm, double *bc, int *okf) {
+    const int lane = threadIdx.x;
     const int G = gridDim.x;
     const unsigned tag = a.tag0 + (unsigned)p;
     u64 *slot = a.gath + (i64)(p & 1) * G * 2;
-    if (threadIdx.x == 0) {
+    double s = sm[0];
+#pragma unroll
+    for (int w = 1; w < RWAVES; ++w) s += sm[w];
+    if (lane == 0) {
         const u64 bits = (u64)__double_as_longlong(s);
         __hip_atomic_store(slot + 2 * blockIdx.x, ((u64)tag << 32) | (unsigned)bits, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(slot + 2 * blockIdx.x + 1, ((u64)tag << 32) | (unsigned)(bits >> 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        const u64 deadline = wall_clock64() + a.timeout;
-        double acc = 0.0;
-        bool all_ok = true;
-        // Lane L holds granule L + 64k of each 512-granule sweep: the lo (even
-        // L) or hi (odd L) half of workgroup c0/2 + L/2 + 32k.
-        for (int c0 = 0; c0 < 2 * G && all_ok; c0 += 512) {
-            unsigned v[8];
-            for (;;) {
-                bool ok = true;
+    const u64 deadline = wall_clock64() + a.timeout;
+    double acc = 0.0;
+    bool all_ok = true;
+    // Lane L holds granule L + 64k of each 512-granule sweep: the lo (even L)
+    // or hi (odd L) half of workgroup c0/2 + L/2 + 32k.
+    for (int c0 = 0; c0 < 2 * G && all_ok; c0 += 512) {
+        unsigned v[8];
+        for (;;) {
+            bool ok = true;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int g = c0 + lane + 64 * k;
-                    v[k] = 0;
-                    if (g < 2 * G) {
-                        const u64 x = __hip_atomic_load(slot + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        v[k] = (unsigned)x;
-                        ok = ok && (unsigned)(x >> 32) == tag;
-                    }
+            for (int k = 0; k < 8; ++k) {
+                const int g = c0 + lane + 64 * k;
+                v[k] = 0;
+                if (g < 2 * G) {
+                    const u64 x = __hip_atomic_load(slot + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    v[k] = (unsigned)x;
+                    ok = ok && (unsigned)(x >> 32) == tag;
                 }
-                if (__all(ok)) break;
-                if (wall_clock64() > deadline) {
-                    all_ok = false;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
             }
+            if (__all(ok)) break;
+            if (wall_clock64() > deadline) {
+                all_ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {  // workgroups in increasing order per lane pair
-                const unsigned o = __shfl_xor(v[k], 1, 64);
-                const unsigned lo = (lane & 1) ? o : v[k], hi = (lane & 1) ? v[k] : o;
-                if (!(lane & 1) && c0 + lane + 64 * k < 2 * G)
-                    acc = acc + __longlong_as_double((long long)(((u64)hi << 32) | lo));
-            }
-        }
-        acc = wave_sum(acc);  // butterfly: the same value on every lane of every workgroup
-        if (all_ok && a.nranks > 1) {
-            const unsigned seq = a.xseq0 + 1u + (unsigned)p, par = seq & 1u;
-            if (blockIdx.x == 0 && lane < 2 * a.nranks) {
-                const int dst = lane >> 1, half = lane & 1;
-                const u64 bits = (u64)__double_as_longlong(acc);
-                xs_put(a.peers.p[dst] + (((i64)par * XS_MAXR + a.rank) * XS_MAXV) * 2 + half, seq,
-                       half ? (unsigned)(bits >> 32) : (unsigned)bits);
-            }
-            unsigned d = 0;
-            bool ok2 = true;
-            if (lane < 2 * a.nranks) {
-                const int src = lane >> 1, half = lane & 1;
-                ok2 = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV) * 2 + half, seq,
-                             wall_clock64() + a.timeout, &d);
-            }
-            all_ok = __all(ok2);
-            double r = 0.0;
-            for (int q = 0; q < a.nranks; ++q) {  // rank order, as k_xchg<XS_SLAB>
-                const unsigned lo = __shfl(d, 2 * q, 64), hi = __shfl(d, 2 * q + 1, 64);
-                const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
-                r = (q == 0) ? v : r + v;
-            }
-            acc = r;
-        }
-        if (lane == 0) {
-            bc[0] = acc;
-            *okf = all_ok ? 1 : 0;
-            if (!all_ok) xs_fail(a.err);
+        for (int k = 0; k < 8; ++k) {  // workgroups in increasing order per lane pair
+            const unsigned o = __shfl_xor(v[k], 1, 64);
+            const unsigned lo = (lane & 1) ? o : v[k], hi = (lane & 1) ? v[k] : o;
+            if (!(lane & 1) && c0 + lane + 64 * k < 2 * G)
+                acc = acc + __longlong_as_double((long long)(((u64)hi << 32) | lo));
         }
     }
-    __syncthreads();
-    tot = bc[0];
-    const bool ok = *okf != 0;
-    __syncthreads();  // bc / okf are rewritten by the next exchange
-    return ok;
+    acc = wave_sum(acc);  // butterfly: the same value on every lane of every workgroup
+    if (all_ok && a.nranks > 1) {
+        const unsigned seq = a.xseq0 + 1u + (unsigned)p, par = seq & 1u;
+        if (blockIdx.x == 0 && lane < 2 * a.nranks) {
+            const int dst = lane >> 1, half = lane & 1;
+            const u64 bits = (u64)__double_as_longlong(acc);
+            xs_put(a.peers.p[dst] + (((i64)par * XS_MAXR + a.rank) * XS_MAXV) * 2 + half, seq,
+                   half ? (unsigned)(bits >> 32) : (unsigned)bits);
+        }
+        unsigned d = 0;
+        bool ok2 = true;
+        if (lane < 2 * a.nranks) {
+            const int src = lane >> 1, half = lane & 1;
+            ok2 = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV) * 2 + half, seq,
+                         wall_clock64() + a.timeout, &d);
+        }
+        all_ok = __all(ok2);
+        double r = 0.0;
+        for (int q = 0; q < a.nranks; ++q) {  // rank order, as k_xchg<XS_SLAB>
+            const unsigned lo = __shfl(d, 2 * q, 64), hi = __shfl(d, 2 * q + 1, 64);
+            const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
+            r = (q == 0) ? v : r + v;
+        }
+        acc = r;
+    }
+    if (lane == 0) {
+        bc[0] = acc;
+        *okf = all_ok ? 1 : 0;
+        if (!all_ok) xs_fail(a.err);
+    }
 }
 
-template <int R2, bool PF, bool NT>
+// R2: register-resident double2 per data thread (w, and the running column);
+// L2: LDS-resident double2 of w per data thread (its two columns stream);
+// PF: the next column is loaded into a third register array before the wait;
+// CW: wave 0 holds no data and only runs the exchange, so its polls never wait
+//     behind prefetch loads (vmcnt retires in issue order).
+template <int R2, int L2, bool PF, bool NT, bool CW>
 __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
+    extern __shared__ double2 lw[];  // L2 > 0: [L2][DT] LDS-resident part of w
     __shared__ double sm[RWAVES];
-    __shared__ double bc[2];
+    __shared__ double bc[1];
     __shared__ int okf;
     __shared__ double hsh[RHMAX + 1];
     constexpr int RB = PF ? R2 : 1;
+    constexpr int DT = CW ? RT - 64 : RT;  // data threads per workgroup
     const int t = threadIdx.x;
+    const bool data = !CW || t >= 64;
+    const int td = CW ? t - 64 : t;
     const int j = a.j, np = 2 * j;
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
-    // Resident layout: workgroup b owns the R2 consecutive chunks of RT double2
-    // starting at chunk b*R2; thread t holds element t of each.  A chunk is
-    // resident when it lies below nres2 (a multiple of RT), so the test is
-    // uniform, and every address is a uniform base (SGPRs) + t*16.
+    // Resident layout in chunks of DT double2 (data thread td holds element td
+    // of each): registers hold chunks b*R2 + k (k < R2), LDS chunks G*R2 + b*L2
+    // + k (k < L2); a chunk is resident when it lies below nres2 (a multiple of
+    // DT), so the test is uniform and every address is a uniform base + td*16.
+    // [nres2, n2) streams through w in HBM as in k_proj.
+    const i64 nch = a.nres2 / DT;
     const i64 c0 = (i64)blockIdx.x * R2;
-    const i64 nchunk = a.nres2 / RT;
+    const i64 l0 = (i64)gridDim.x * R2 + (i64)blockIdx.x * L2;
     const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
     double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
-    auto colchunk = [&](int col, int k) { return V2 + (i64)col * ld2 + (c0 + k) * RT; };
+    auto colchunk = [&](int col, i64 c) { return V2 + (i64)col * ld2 + c * DT; };
     double2 wr[R2], xa[R2], xb[RB];
 #pragma unroll
     for (int k = 0; k < R2; ++k) {  // zeros past nres2: they add exact zeros to every dot
         wr[k] = xa[k] = double2{0.0, 0.0};
         if constexpr (PF) xb[k] = double2{0.0, 0.0};
-        if (c0 + k < nchunk) {
-            wr[k] = W2[(c0 + k) * RT + t];
-            xa[k] = colchunk(0, k)[t];                         // V(:,1): AXPY partner of projection 0
-            if constexpr (PF) xb[k] = colchunk(1 % j, k)[t];  // its dot partner
+        if (data && c0 + k < nch) {
+            wr[k] = W2[(c0 + k) * DT + td];
+            xa[k] = colchunk(0, c0 + k)[td];                         // V(:,1): AXPY partner of projection 0
+            if constexpr (PF) xb[k] = colchunk(1 % j, c0 + k)[td];  // its dot partner
         }
+    }
+    if constexpr (L2 > 0) {
+        for (int k = 0; k < L2; ++k)
+            if (data && l0 + k < nch) lw[k * DT + td] = W2[(l0 + k) * DT + td];
     }
     double h;
     {
@@ -1097,12 +1111,11 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         for (int k = t; k < a.npin; k += RT) s += a.pin[k];
         h = block_sum_rt(s, sm);
     }
-    // streamed part [nres2, n2): grid-stride like k_proj, two double2 per array in flight
-    const i64 sstride = (i64)gridDim.x * RT;
-    const i64 sbase = a.nres2 + (i64)blockIdx.x * RT + t;
+    const i64 sstride = (i64)gridDim.x * DT;
+    const i64 sbase = a.nres2 + (i64)blockIdx.x * DT + td;
     // Projection p: i = p mod j, AXPY w -= h V_i (h = the dot of p), then the
     // dot of projection p+1 with V_q, q = (p+1) mod j -- or ||w||^2 after the
-    // last one.  X holds V_i; PF: Y holds V_q (prefetched), then X <- the dot
+    // last one.  X holds V_i; PF: Y holds V_q (prefetched), and X <- the dot
     // partner of p+1 is loaded before the wait.
     auto proj = [&](int p, auto &X, auto &Y) -> bool {
         const int i = p % j;
@@ -1110,79 +1123,116 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         const int q = last ? i : (p + 1) % j;
         if (blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
         double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < R2; ++k) {
-            wr[k].x = wr[k].x - h * X[k].x;
-            wr[k].y = wr[k].y - h * X[k].y;
-        }
-        if (last) {
+        if (data) {
 #pragma unroll
             for (int k = 0; k < R2; ++k) {
-                acc = acc + wr[k].x * wr[k].x;
-                acc = acc + wr[k].y * wr[k].y;
+                wr[k].x = wr[k].x - h * X[k].x;
+                wr[k].y = wr[k].y - h * X[k].y;
             }
-        } else if constexpr (PF) {
+            if (last) {
 #pragma unroll
-            for (int k = 0; k < R2; ++k) {
-                acc = acc + wr[k].x * Y[k].x;
-                acc = acc + wr[k].y * Y[k].y;
-            }
-        } else {
+                for (int k = 0; k < R2; ++k) {
+                    acc = acc + wr[k].x * wr[k].x;
+                    acc = acc + wr[k].y * wr[k].y;
+                }
+            } else if constexpr (PF) {
 #pragma unroll
-            for (int k = 0; k < R2; ++k)
-                if (c0 + k < nchunk) X[k] = ldv<NT>(colchunk(q, k) + t);
+                for (int k = 0; k < R2; ++k) {
+                    acc = acc + wr[k].x * Y[k].x;
+                    acc = acc + wr[k].y * Y[k].y;
+                }
+            } else {
 #pragma unroll
-            for (int k = 0; k < R2; ++k) {
-                acc = acc + wr[k].x * X[k].x;
-                acc = acc + wr[k].y * X[k].y;
-            }
-        }
-        const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
-        const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
-        for (i64 e0 = sbase; e0 < n2; e0 += 2 * sstride) {
-            double2 wv[2], av[2], bv[2];
+                for (int k = 0; k < R2; ++k)
+                    if (c0 + k < nch) X[k] = ldv<NT>(colchunk(q, c0 + k) + td);
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const i64 e = e0 + u * sstride;
-                if (e < n2) {
-                    wv[u] = W2[e];
-                    av[u] = ldv<NT>(A2 + e);
-                    if (!last) bv[u] = ldv<NT>(B2 + e);
+                for (int k = 0; k < R2; ++k) {
+                    acc = acc + wr[k].x * X[k].x;
+                    acc = acc + wr[k].y * X[k].y;
                 }
             }
+            const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
+            const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
+            if constexpr (L2 > 0) {  // w in LDS, its two columns stream: 16 B/unknown
+                for (int k = 0; k < L2; k += 2) {
+                    double2 wv[2], av[2], bv[2];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const i64 e = e0 + u * sstride;
-                if (e < n2) {
-                    wv[u].x = wv[u].x - h * av[u].x;
-                    wv[u].y = wv[u].y - h * av[u].y;
-                    W2[e] = wv[u];
-                    if (last) {
-                        acc = acc + wv[u].x * wv[u].x;
-                        acc = acc + wv[u].y * wv[u].y;
-                    } else {
-                        acc = acc + wv[u].x * bv[u].x;
-                        acc = acc + wv[u].y * bv[u].y;
+                    for (int u = 0; u < 2; ++u) {
+                        const i64 c = l0 + k + u;
+                        if (k + u < L2 && c < nch) {
+                            wv[u] = lw[(k + u) * DT + td];
+                            av[u] = ldv<NT>(A2 + c * DT + td);
+                            if (!last) bv[u] = ldv<NT>(B2 + c * DT + td);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const i64 c = l0 + k + u;
+                        if (k + u < L2 && c < nch) {
+                            wv[u].x = wv[u].x - h * av[u].x;
+                            wv[u].y = wv[u].y - h * av[u].y;
+                            lw[(k + u) * DT + td] = wv[u];
+                            if (last) {
+                                acc = acc + wv[u].x * wv[u].x;
+                                acc = acc + wv[u].y * wv[u].y;
+                            } else {
+                                acc = acc + wv[u].x * bv[u].x;
+                                acc = acc + wv[u].y * bv[u].y;
+                            }
+                        }
                     }
                 }
             }
+            for (i64 e0 = sbase; e0 < n2; e0 += 2 * sstride) {  // streamed part: 32 B/unknown
+                double2 wv[2], av[2], bv[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const i64 e = e0 + u * sstride;
+                    if (e < n2) {
+                        wv[u] = W2[e];
+                        av[u] = ldv<NT>(A2 + e);
+                        if (!last) bv[u] = ldv<NT>(B2 + e);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const i64 e = e0 + u * sstride;
+                    if (e < n2) {
+                        wv[u].x = wv[u].x - h * av[u].x;
+                        wv[u].y = wv[u].y - h * av[u].y;
+                        W2[e] = wv[u];
+                        if (last) {
+                            acc = acc + wv[u].x * wv[u].x;
+                            acc = acc + wv[u].y * wv[u].y;
+                        } else {
+                            acc = acc + wv[u].x * bv[u].x;
+                            acc = acc + wv[u].y * bv[u].y;
+                        }
+                    }
+                }
+            }
+            if ((a.n & 1) && blockIdx.x == 0 && td == 0) {  // odd-length tail element
+                const i64 e = a.n - 1;
+                const double x = a.w[e] - h * a.V[(i64)i * a.ld + e];
+                a.w[e] = x;
+                acc = acc + (last ? x * x : x * a.V[(i64)q * a.ld + e]);
+            }
         }
-        if ((a.n & 1) && blockIdx.x == 0 && t == 0) {  // odd-length tail element
-            const i64 e = a.n - 1;
-            const double x = a.w[e] - h * a.V[(i64)i * a.ld + e];
-            a.w[e] = x;
-            acc = acc + (last ? x * x : x * a.V[(i64)q * a.ld + e]);
-        }
-        const double s = block_sum_rt(acc, sm);
+        acc = wave_sum(acc);
+        if ((t & 63) == 0) sm[t >> 6] = acc;
+        __syncthreads();
         if constexpr (PF) {
-            if (p + 2 < np) {  // the dot partner of projection p+1, before the wait
+            if (data && p + 2 < np) {  // the dot partner of projection p+1, in flight during the exchange
                 const int q2 = (p + 2) % j;
 #pragma unroll
                 for (int k = 0; k < R2; ++k)
-                    if (c0 + k < nchunk) X[k] = ldv<NT>(colchunk(q2, k) + t);
+                    if (c0 + k < nch) X[k] = ldv<NT>(colchunk(q2, c0 + k) + td);
             }
         }
-        return res_allreduce(a, p, s, h, bc, &okf);
+        if (t < 64) res_exchange(a, p, sm, bc, &okf);
+        __syncthreads();
+        h = bc[0];
+        return okf != 0;
     };
     bool ok = true;
     if constexpr (PF) {
@@ -1197,15 +1247,24 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
     // h = ||w|| ; V(:,j+1) = w / h  (h == 0: zeros, as k_scale)
     const double hn = sqrt(h);
     double2 *__restrict__ O2 = reinterpret_cast<double2 *>(a.vout);
+    if (data) {
 #pragma unroll
-    for (int k = 0; k < R2; ++k)
-        if (c0 + k < nchunk)
-            O2[(c0 + k) * RT + t] = hn != 0.0 ? double2{wr[k].x / hn, wr[k].y / hn} : double2{0.0, 0.0};
-    for (i64 e = sbase; e < n2; e += sstride) {
-        const double2 v = W2[e];
-        O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
+        for (int k = 0; k < R2; ++k)
+            if (c0 + k < nch)
+                O2[(c0 + k) * DT + td] = hn != 0.0 ? double2{wr[k].x / hn, wr[k].y / hn} : double2{0.0, 0.0};
+        if constexpr (L2 > 0) {
+            for (int k = 0; k < L2; ++k)
+                if (l0 + k < nch) {
+                    const double2 v = lw[k * DT + td];
+                    O2[(l0 + k) * DT + td] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
+                }
+        }
+        for (i64 e = sbase; e < n2; e += sstride) {
+            const double2 v = W2[e];
+            O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
+        }
+        if ((a.n & 1) && blockIdx.x == 0 && td == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     }
-    if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     if (blockIdx.x == 0) {  // H(1:j+1, j) to the device column and the mapped host mirror
         __syncthreads();
         for (int k = t; k < j; k += RT) {

@@ -224,11 +224,14 @@ int gk_sync(gk_ctx *ctx);
  *                          m <= 512, one context per device), 1 also with several contexts on one
  *                          device (their streams must then run concurrently), 0 off (one launch
  *                          per projection)
- *   GK_TUNE_RES_R2         cap of register-resident double2 per thread and array: 0 auto, 2/4/8/16
+ *   GK_TUNE_RES_R2         cap of register-resident double2 per thread and array: 0 auto, 2/4/8/12
  *   GK_TUNE_RES_SHARE      contexts sharing this device (resident launches use CUs / share
  *                          workgroups; gk_comm_init_local sets it to the group size)
  *   GK_TUNE_RES_TIMEOUT_MS deadline of one in-launch wait (default 20000); a miss fails the step
- *                          with GK_ERR_COMM and switches the context to the launch path */
+ *                          with GK_ERR_COMM and switches the context to the launch path
+ *   GK_TUNE_RES_LDS        1 (default): when the slab exceeds the register-resident part, keep w
+ *                          of 144 KiB more per workgroup in LDS (16 B/unknown per projection
+ *                          instead of 32); 0: stream it */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
@@ -241,6 +244,7 @@ int gk_sync(gk_ctx *ctx);
 #define GK_TUNE_RES_R2 9
 #define GK_TUNE_RES_SHARE 10
 #define GK_TUNE_RES_TIMEOUT_MS 11
+#define GK_TUNE_RES_LDS 12
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

@@ -12,10 +12,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _single(N, m, method, prec, degree, max_cycles):
+def _single(N, m, method, prec, degree, max_cycles, res=-1):
     import gmres_amd as ga
 
     with ga.Context(N, m) as c:
+        c.tune(8, res)  # GK_TUNE_RES: -1 auto; 0 = the launch-per-projection path
         c.set_precond(prec, (8.2, 0.2), degree)
         c.set_rhs_ones()
         return _solve(c, method, prec, max_cycles)
@@ -132,7 +133,7 @@ def test_rccl_one_rank_communicator(monkeypatch, method, prec):
     import gmres_amd as ga
 
     N, m = 64, 16
-    ref = _single(N, m, method, prec, 1, 4)
+    ref = _single(N, m, method, prec, 1, 4, res=0)  # same kernels (RCCL cannot drive the resident step)
     monkeypatch.setenv("GK_FORCE_RCCL", "1")
     with ga.Context(N, m) as c:
         c.comm_init(1, 0, N, ga.Context.unique_id())

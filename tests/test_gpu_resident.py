@@ -42,7 +42,7 @@ CASES = [
     (64, 20, "identity", 0, 1),      # fully resident, R2 = 2, prefetch
     (130, 30, "cbpr2", 2, 8),        # 32 workgroups x 512 x 2 < n/2: streamed tail of the vector
     (45, 12, "identity", 2, 64),     # odd N: the tail element, 4 workgroups
-    (256, 40, "cheb", 16, 16),       # two-array variant
+    (256, 40, "cheb", 12, 16),       # two-array variant (+ LDS-resident w)
     (200, 25, "identity", 4, 32),    # R2 = 4 with a streamed part
     (512, 30, "identity", 8, 4),     # R2 = 8, fully resident
 ]
