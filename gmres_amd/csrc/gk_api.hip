@@ -134,6 +134,7 @@ struct gk_ctx {
     int tune_res = -1;                              // -1 auto, 0 off, 1 on where possible
     int tune_res_r2 = 0;                            // cap of resident double2 per thread (0 = auto)
     int tune_res_lds = 1;                           // LDS-resident part of w for large slabs
+    int tune_res_wonly = -1;                        // large slabs: w-only variant (-1: by the byte model)
     int res_share = 1;                              // contexts sharing this device's CUs
     int res_timeout_ms = 20000;
     bool res_broken = false;                        // a deadline was missed: launch path from then on
@@ -568,12 +569,26 @@ constexpr int RES_LDS_MIN = 96 * 1024;  // dynamic LDS: > half a CU's 160 KiB, s
 constexpr int RES_L2 = 18;              // LDS-resident double2 of w per data thread (18 x 512 x 16 B = 144 KiB)
 constexpr int RES_R2_BIG = 12;          // two register arrays of 12 double2 fit 256 VGPRs without spills
 
+constexpr int RES_RW = 64, RES_LW = 36;  // w-only variant: double2 of w per thread in registers / LDS
+
 struct ResPlan {
     int G = 0, r2 = 0, l2 = 0;
-    bool pf = false, nt = false, cw = false;
+    bool pf = false, nt = false, cw = false, wo = false;
     i64 nres2 = 0;
     int lds = 0;
 };
+
+// Modelled fabric bytes per projection (per double2) of the two large-slab
+// variants: pairs (w + running column, 8 B/unknown) in 2 x 12 registers + w in
+// LDS (16 B) vs w only in registers + LDS (16 B); the rest streams (32 B).
+bool wonly_pays(i64 n2, int G) {
+    const i64 rp = (i64)G * RES_R2_BIG * gk::RT, lp = (i64)G * RES_L2 * gk::RT;
+    const i64 rw = (i64)G * (RES_RW + RES_LW) * gk::WT;
+    auto clamp = [](i64 v) { return v < 0 ? (i64)0 : v; };
+    const i64 pr = std::min(n2, rp), pl = std::min(clamp(n2 - rp), lp), ps = clamp(n2 - rp - lp);
+    const i64 wr = std::min(n2, rw), ws = clamp(n2 - rw);
+    return 16 * wr + 32 * ws < 8 * pr + 16 * pl + 32 * ps;
+}
 
 // Can step j run as one resident launch, and with which variant?  Needs an
 // in-launch reduction path: single rank, or the device exchange (RCCL and the
@@ -605,6 +620,14 @@ bool res_plan(gk_ctx *c, ResPlan &p) {
         p.G = gcw;
         p.pf = p.cw = true;
         p.nres2 = std::min<i64>(n2 / dcw * dcw, (i64)p.G * p.r2 * dcw);
+    } else if (c->tune_res_wonly > 0 || (c->tune_res_wonly < 0 && wonly_pays(n2, gmax))) {
+        // w only, one wave per SIMD: 16 B/unknown per projection for ~100 chunks per workgroup
+        p.G = gmax;
+        p.wo = true;
+        const i64 dt = gk::WT;
+        p.nres2 = std::min<i64>(n2 / dt * dt, (i64)p.G * (RES_RW + RES_LW) * dt);
+        p.lds = RES_LW * gk::WT * (int)sizeof(double2);
+        return true;
     } else {
         p.G = gmax;
         p.r2 = RES_R2_BIG;
@@ -630,7 +653,20 @@ int launch_res_t(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     return GK_OK;
 }
 
+int launch_wres(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    static std::atomic<int> attr{0};
+    if (attr.load() < p.lds) {
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RES_RW, RES_LW>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
+        attr = p.lds;
+    }
+    gk::k_mgs_wres<RES_RW, RES_LW><<<p.G, gk::WT, p.lds, c->st>>>(a);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
 int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    if (p.wo) return launch_wres(c, p, a);
 #define GK_RES_CASE(R, L, PFV, CWV)                                                                 \
     if (p.r2 == R && p.l2 == L && p.pf == PFV && p.cw == CWV)                                      \
         return p.nt ? launch_res_t<R, L, PFV, true, CWV>(c, p, a) : launch_res_t<R, L, PFV, false, CWV>(c, p, a);
@@ -1708,6 +1744,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
             c->res_share = value;
             break;
         case GK_TUNE_RES_LDS: c->tune_res_lds = value != 0; break;
+        case GK_TUNE_RES_WONLY: c->tune_res_wonly = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
             c->res_timeout_ms = value;

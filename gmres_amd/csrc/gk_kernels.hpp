@@ -979,6 +979,7 @@ __device__ __forceinline__ double block_sum_rt(double v, double *sm) {
 // G partials of the grid (8 granules in flight per lane) and sum them in a
 // fixed order; on N ranks then add the rank totals in rank order.  Result in
 // bc[0]; *okf = 0 when a deadline passed (then *err is set).
+template <int NW = RWAVES>
 __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const double *sm, double *bc, int *okf) {
     const int lane = threadIdx.x;
     const int G = gridDim.x;
@@ -986,7 +987,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
     u64 *slot = a.gath + (i64)(p & 1) * G * 2;
     double s = sm[0];
 #pragma unroll
-    for (int w = 1; w < RWAVES; ++w) s += sm[w];
+    for (int w = 1; w < NW; ++w) s += sm[w];
     if (lane == 0) {
         const u64 bits = (u64)__double_as_longlong(s);
         __hip_atomic_store(slot + 2 * blockIdx.x, ((u64)tag << 32) | (unsigned)bits, __ATOMIC_RELAXED,
@@ -1268,6 +1269,191 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
     if (blockIdx.x == 0) {  // H(1:j+1, j) to the device column and the mapped host mirror
         __syncthreads();
         for (int k = t; k < j; k += RT) {
+            a.hs[k] = hsh[k];
+            a.hcopy[k] = hsh[k];
+        }
+        if (t == 0) {
+            a.hs[j] = hn;
+            a.hcopy[j] = hn;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// Resident MGS-R step, w-only variant for large slabs: ONE wave per SIMD
+// (256-thread workgroups, one per CU) so each lane can hold ~400 registers
+// (VGPRs + AGPRs of the unified file), and they hold w only -- RW double2 per
+// thread in registers and LW more in LDS.  Per projection a resident unknown
+// moves 16 B (its two Krylov columns) instead of 32; the running column V_q is
+// loaded with the default policy, so it is still in the Infinity Cache when
+// it is read again as V_i by the next projection (V_i itself non-temporal).
+// Same exchange, same arithmetic as k_mgs_res.
+// --------------------------------------------------------------------------
+constexpr int WT = 256;  // threads per workgroup (4 waves, one per SIMD)
+constexpr int WB = 8;    // double2 per column per batch in flight per thread
+
+template <int RW, int LW>
+__global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
+    extern __shared__ double2 lw[];  // [LW][WT]
+    __shared__ double sm[WT / 64];
+    __shared__ double bc[1];
+    __shared__ int okf;
+    __shared__ double hsh[RHMAX + 1];
+    const int t = threadIdx.x;
+    const int j = a.j, np = 2 * j;
+    const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
+    const i64 nch = a.nres2 / WT;
+    const i64 c0 = (i64)blockIdx.x * RW;
+    const i64 l0 = (i64)gridDim.x * RW + (i64)blockIdx.x * LW;
+    const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
+    double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
+    double2 wr[RW];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < nch) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
+    for (int k = 0; k < LW; ++k)
+        if (l0 + k < nch) lw[k * WT + t] = W2[(l0 + k) * WT + t];
+    double h;
+    {
+        double s = 0.0;
+        for (int k = t; k < a.npin; k += WT) s += a.pin[k];
+        s = wave_sum(s);
+        if ((t & 63) == 0) sm[t >> 6] = s;
+        __syncthreads();
+        h = sm[0];
+#pragma unroll
+        for (int w = 1; w < WT / 64; ++w) h += sm[w];
+        __syncthreads();
+    }
+    const i64 sstride = (i64)gridDim.x * WT;
+    const i64 sbase = a.nres2 + (i64)blockIdx.x * WT + t;
+    bool ok = true;
+    for (int p = 0; p < np && ok; ++p) {
+        const int i = p % j;
+        const bool last = p == np - 1;
+        const int q = last ? i : (p + 1) % j;
+        if (blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
+        const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
+        const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
+        double acc = 0.0;
+        // registers: batches of WB chunks, both columns in flight
+#pragma unroll
+        for (int k0 = 0; k0 < RW; k0 += WB) {
+            double2 av[WB], bv[WB];
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                const i64 c = c0 + k0 + u;
+                if (k0 + u < RW && c < nch) {
+                    av[u] = ldv<true>(A2 + c * WT + t);
+                    if (!last) bv[u] = B2[c * WT + t];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                const int k = k0 + u;
+                if (k < RW && c0 + k < nch) {
+                    wr[k].x = wr[k].x - h * av[u].x;
+                    wr[k].y = wr[k].y - h * av[u].y;
+                    if (last) {
+                        acc = acc + wr[k].x * wr[k].x;
+                        acc = acc + wr[k].y * wr[k].y;
+                    } else {
+                        acc = acc + wr[k].x * bv[u].x;
+                        acc = acc + wr[k].y * bv[u].y;
+                    }
+                }
+            }
+        }
+        // LDS: the same, w from / to LDS
+        for (int k0 = 0; k0 < LW; k0 += WB) {
+            double2 av[WB], bv[WB];
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                const i64 c = l0 + k0 + u;
+                if (k0 + u < LW && c < nch) {
+                    av[u] = ldv<true>(A2 + c * WT + t);
+                    if (!last) bv[u] = B2[c * WT + t];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                const int k = k0 + u;
+                if (k < LW && l0 + k < nch) {
+                    double2 wv = lw[k * WT + t];
+                    wv.x = wv.x - h * av[u].x;
+                    wv.y = wv.y - h * av[u].y;
+                    lw[k * WT + t] = wv;
+                    if (last) {
+                        acc = acc + wv.x * wv.x;
+                        acc = acc + wv.y * wv.y;
+                    } else {
+                        acc = acc + wv.x * bv[u].x;
+                        acc = acc + wv.y * bv[u].y;
+                    }
+                }
+            }
+        }
+        for (i64 e0 = sbase; e0 < n2; e0 += 2 * sstride) {  // streamed part: 32 B/unknown
+            double2 wv[2], av[2], bv[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const i64 e = e0 + u * sstride;
+                if (e < n2) {
+                    wv[u] = W2[e];
+                    av[u] = ldv<true>(A2 + e);
+                    if (!last) bv[u] = B2[e];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const i64 e = e0 + u * sstride;
+                if (e < n2) {
+                    wv[u].x = wv[u].x - h * av[u].x;
+                    wv[u].y = wv[u].y - h * av[u].y;
+                    W2[e] = wv[u];
+                    if (last) {
+                        acc = acc + wv[u].x * wv[u].x;
+                        acc = acc + wv[u].y * wv[u].y;
+                    } else {
+                        acc = acc + wv[u].x * bv[u].x;
+                        acc = acc + wv[u].y * bv[u].y;
+                    }
+                }
+            }
+        }
+        if ((a.n & 1) && blockIdx.x == 0 && t == 0) {  // odd-length tail element
+            const i64 e = a.n - 1;
+            const double x = a.w[e] - h * a.V[(i64)i * a.ld + e];
+            a.w[e] = x;
+            acc = acc + (last ? x * x : x * a.V[(i64)q * a.ld + e]);
+        }
+        acc = wave_sum(acc);
+        if ((t & 63) == 0) sm[t >> 6] = acc;
+        __syncthreads();
+        if (t < 64) res_exchange<WT / 64>(a, p, sm, bc, &okf);
+        __syncthreads();
+        h = bc[0];
+        ok = okf != 0;
+    }
+    if (!ok) return;  // uniform per workgroup; *err is set
+    const double hn = sqrt(h);
+    double2 *__restrict__ O2 = reinterpret_cast<double2 *>(a.vout);
+#pragma unroll
+    for (int k = 0; k < RW; ++k)
+        if (c0 + k < nch)
+            O2[(c0 + k) * WT + t] = hn != 0.0 ? double2{wr[k].x / hn, wr[k].y / hn} : double2{0.0, 0.0};
+    for (int k = 0; k < LW; ++k)
+        if (l0 + k < nch) {
+            const double2 v = lw[k * WT + t];
+            O2[(l0 + k) * WT + t] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
+        }
+    for (i64 e = sbase; e < n2; e += sstride) {
+        const double2 v = W2[e];
+        O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
+    }
+    if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
+    if (blockIdx.x == 0) {
+        __syncthreads();
+        for (int k = t; k < j; k += WT) {
             a.hs[k] = hsh[k];
             a.hcopy[k] = hsh[k];
         }

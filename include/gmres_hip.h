@@ -231,7 +231,10 @@ int gk_sync(gk_ctx *ctx);
  *                          with GK_ERR_COMM and switches the context to the launch path
  *   GK_TUNE_RES_LDS        1 (default): when the slab exceeds the register-resident part, keep w
  *                          of 144 KiB more per workgroup in LDS (16 B/unknown per projection
- *                          instead of 32); 0: stream it */
+ *                          instead of 32); 0: stream it
+ *   GK_TUNE_RES_WONLY      large slabs: -1 (default) pick by the modelled bytes per projection,
+ *                          1 always, 0 never the w-only variant (one wave per SIMD, ~490 registers
+ *                          per lane: w in registers + LDS, both columns streamed) */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
@@ -245,6 +248,7 @@ int gk_sync(gk_ctx *ctx);
 #define GK_TUNE_RES_SHARE 10
 #define GK_TUNE_RES_TIMEOUT_MS 11
 #define GK_TUNE_RES_LDS 12
+#define GK_TUNE_RES_WONLY 13
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

@@ -19,11 +19,12 @@ pytestmark = pytest.mark.gpu
 T_RES, T_R2, T_SHARE, T_TMO = 8, 9, 10, 11
 
 
-def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False):
+def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False, wonly=-1):
     import gmres_amd as ga
 
     with ga.Context(N, m) as c:
         c.tune(T_RES, res)
+        c.tune(13, wonly)  # GK_TUNE_RES_WONLY
         c.tune(T_R2, r2)
         c.tune(T_SHARE, share)
         c.tune(T_TMO, 5000)
@@ -48,10 +49,17 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("N,m,prec,r2,share", CASES)
-def test_resident_matches_launch_path(N, m, prec, r2, share):
+WCASES = [  # w-only variant (one wave per SIMD): few workgroups so the LDS and streamed parts are used
+    (300, 20, "identity", 12, 64),
+    (181, 16, "cbpr2", 12, 128),     # odd N
+    (512, 24, "cheb", 12, 32),
+]
+
+
+@pytest.mark.parametrize("N,m,prec,r2,share,wonly", [c + (-1,) for c in CASES] + [c + (1,) for c in WCASES])
+def test_resident_matches_launch_path(N, m, prec, r2, share, wonly):
     ref, _ = _run(N, m, prec, res=0)
-    got, prof = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True)
+    got, prof = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True, wonly=wonly)
     # the resident kernel ran every step (k_proj only in the off-cycle diagnostics)
     assert prof["res"][1] > 0 and prof["proj"][1] < prof["res"][1] // 4, prof
     assert got.n_cycles == ref.n_cycles

@@ -16,8 +16,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KEYS = {"nt": 0, "pj": 1, "st": 2, "rev": 3, "blk": 4, "unr": 5, "cf": 6, "res": 8, "rr2": 9, "lds": 12}
-DEFAULTS = {0: -1, 1: 0, 2: 0, 3: 0, 4: 0, 5: 0, 6: 1, 8: -1, 9: 0, 12: 1}
+KEYS = {"nt": 0, "pj": 1, "st": 2, "rev": 3, "blk": 4, "unr": 5, "cf": 6, "res": 8, "rr2": 9, "lds": 12, "wo": 13}
+DEFAULTS = {0: -1, 1: 0, 2: 0, 3: 0, 4: 0, 5: 0, 6: 1, 8: -1, 9: 0, 12: 1, 13: -1}
 
 
 def parse_variant(s: str) -> dict:
