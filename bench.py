@@ -249,19 +249,33 @@ def main() -> None:
         if prof and prof.get("res", (0.0, 0))[1] > 0:
             # resident MGS-R step: one launch = the 2j projections + norm + scale of step j
             ms, launches = prof["res"]
-            S = max(1, args.prof_every)
-            steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
-            palg = float(sum(res_alg_bytes(nloc, j) for j in steps_js))
+            if args.method == "hh":
+                # every launch sampled (profile(1)): per step j a RES_HH_DOWN chain (v_j = P_1..P_j e_j)
+                # and a RES_HH_UP chain (w = P_j..P_1 A v_j), j reflections of 40n each
+                # (gmres_hh.f90:269-304); per cycle one more chain of n_out = m (x update, :361-373)
+                steps_js = list(range(1, m + 1)) * cycles
+                palg = float(sum(2 * j * 40 * nloc for j in steps_js) + cycles * m * 40 * nloc)
+                nproj = sum(2 * j for j in steps_js) + cycles * m
+                kname = ("gk::k_mgs_res / k_mgs_wres in reflection mode (RES_HH_DOWN / RES_HH_UP: a chain of j "
+                         "Householder reflections, one persistent launch per chain)")
+                timing = "HIP events on the context stream around every resident launch of the timed cycles"
+            else:
+                S = max(1, args.prof_every)
+                steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
+                palg = float(sum(res_alg_bytes(nloc, j) for j in steps_js))
+                nproj = sum(2 * j + 1 for j in steps_js)
+                kname = ("gk::k_mgs_res (resident MGS-R step: 2j fused projections + norm + scale, one "
+                         "persistent launch per Arnoldi step)")
+                timing = (f"HIP events on the context stream around the step launch of steps j % {S} == 0 "
+                          f"of the timed cycles")
             achieved = palg / (ms / 1e3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "kernel": "gk::k_mgs_res (resident MGS-R step: 2j fused projections + norm + scale, one "
-                              "persistent launch per Arnoldi step)",
+                    "kernel": kname,
                     "launches": launches, "avg_launch_us": round(ms * 1e3 / launches, 2),
                     "alg_bytes_per_launch": round(palg / launches),
-                    "per_projection_us": round(ms * 1e3 / sum(2 * j + 1 for j in steps_js), 2),
-                    "timing": f"HIP events on the context stream around the step launch of steps j % {S} == 0 "
-                              f"of the timed cycles",
+                    "per_projection_us": round(ms * 1e3 / nproj, 2),
+                    "timing": timing,
                     "per_kernel_ms_sampled": {k: round(v[0], 3) for k, v in prof.items()}}
             tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
             key = f"{N}_{m}_{args.prec}_{args.method}_{world}_res"

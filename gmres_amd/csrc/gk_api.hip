@@ -640,29 +640,47 @@ bool res_plan(gk_ctx *c, ResPlan &p) {
     return true;
 }
 
-template <int R2, int L2, bool PF, bool NT, bool CW>
-int launch_res_t(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+template <int R2, int L2, bool PF, bool NT, bool CW, int MODE>
+int launch_res_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     static std::atomic<int> attr{0};
     if (attr.load() < p.lds) {
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_res<R2, L2, PF, NT, CW>),
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_res<R2, L2, PF, NT, CW, MODE>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
         attr = p.lds;
     }
-    gk::k_mgs_res<R2, L2, PF, NT, CW><<<p.G, gk::RT, p.lds, c->st>>>(a);
+    gk::k_mgs_res<R2, L2, PF, NT, CW, MODE><<<p.G, gk::RT, p.lds, c->st>>>(a);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
+template <int R2, int L2, bool PF, bool NT, bool CW>
+int launch_res_t(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    switch (a.mode) {
+        case gk::RES_HH_UP: return launch_res_m<R2, L2, PF, NT, CW, gk::RES_HH_UP>(c, p, a);
+        case gk::RES_HH_DOWN: return launch_res_m<R2, L2, PF, NT, CW, gk::RES_HH_DOWN>(c, p, a);
+        default: return launch_res_m<R2, L2, PF, NT, CW, gk::RES_MGS>(c, p, a);
+    }
+}
+
+template <int MODE>
+int launch_wres_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    static std::atomic<int> attr{0};
+    if (attr.load() < p.lds) {
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RES_RW, RES_LW, MODE>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
+        attr = p.lds;
+    }
+    gk::k_mgs_wres<RES_RW, RES_LW, MODE><<<p.G, gk::WT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
 }
 
 int launch_wres(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
-    static std::atomic<int> attr{0};
-    if (attr.load() < p.lds) {
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RES_RW, RES_LW>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
-        attr = p.lds;
+    switch (a.mode) {
+        case gk::RES_HH_UP: return launch_wres_m<gk::RES_HH_UP>(c, p, a);
+        case gk::RES_HH_DOWN: return launch_wres_m<gk::RES_HH_DOWN>(c, p, a);
+        default: return launch_wres_m<gk::RES_MGS>(c, p, a);
     }
-    gk::k_mgs_wres<RES_RW, RES_LW><<<p.G, gk::WT, p.lds, c->st>>>(a);
-    LAUNCHCHK();
-    return GK_OK;
 }
 
 int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
@@ -679,17 +697,24 @@ int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     return set_err(GK_ERR_ARG, "no resident variant for r2=%d l2=%d", p.r2, p.l2);
 }
 
-// The MGS cascade of step j + norm + scale as one launch; pin/npin = the
-// (all-reduced) partial slab of the first dot <w, V(:,1)>.
-int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, double *hs, double *hcopy) {
+// One resident launch (gk::ResArgs::mode):
+//  RES_MGS: the MGS cascade of step j + norm + scale; pin/npin = the
+//    (all-reduced) partial slab of the first dot <w, V(:,1)>; H column to hs/hcopy.
+//  RES_HH_UP: w = P_j..P_1 w (pin = <w, P_1>); hs[0] = ||w(j+1:n)||^2.
+//  RES_HH_DOWN: w = P_1..P_j w (no pin).
+int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, double *hs, double *hcopy,
+             int mode = gk::RES_MGS, double *w = nullptr) {
     ProfScope ps(c, GK_KID_RES);
-    const int np = 2 * j;
+    const int np = mode == gk::RES_MGS ? 2 * j : j;  // exchanges of the launch
     if (c->res_tag > 0xF0000000u) {  // tags must never repeat within the granule region's lifetime
         HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * 4 * gk::RGMAX, c->st));
         c->res_tag = 1;
     }
     gk::ResArgs a{};
-    a.w = c->w;
+    a.w = w != nullptr ? w : c->w;
+    a.mode = mode;
+    a.coef = mode == gk::RES_MGS ? 1.0 : 2.0;
+    a.tail0 = mode == gk::RES_HH_UP ? (i64)j - c->g0 : 0;
     a.V = c->V;
     a.vout = c->V + (i64)j * c->ld;
     a.ld = c->ld;
@@ -959,6 +984,8 @@ int gram(gk_ctx *c, const double *base, int ncols, std::vector<double> &G) {
 // calculate_verr :581-585).  The chain's first launch is a pure dot.
 int reflect_chain_down(gk_ctx *c, double *v, int k) {
     double *P = c->V;
+    ResPlan rp;
+    if (res_plan(c, rp)) return res_step(c, k, rp, nullptr, 0, nullptr, nullptr, gk::RES_HH_DOWN, v);
     int s0 = 0, s1 = 1;
     CHK(proj(c, gk::PJ_DOT, v, nullptr, P + (i64)(k - 1) * c->ld, nullptr, 0, slot(c, s0), nullptr, 2.0));
     int np = c->np_pj;
@@ -1606,20 +1633,29 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
         CHK(stencil(c, gk::OP_PLAIN, gk::ACC_DOT, a));
     }
     int np = c->last_np;
-    // w = P_j .. P_1 w ; the last reflection also accumulates ||w(j+1:n)||^2
-    for (int i = 1; i <= j; ++i) {
+    ResPlan rp;
+    if (res_plan(c, rp)) {  // w = P_j .. P_1 w and ||w(j+1:n)||^2 as one resident launch
         CHK(allreduce(c, slot(c, s0), np));
-        const double *va = P + (i64)(i - 1) * ld;
-        if (i < j) {
-            CHK(proj(c, gk::PJ_AXPY_DOT, c->w, va, P + (i64)i * ld, slot(c, s0), np, slot(c, s1), nullptr, 2.0));
-        } else {
-            CHK(proj(c, gk::PJ_AXPY_NORM, c->w, va, nullptr, slot(c, s0), np, slot(c, s1), nullptr, 2.0,
-                     (i64)j - c->g0));
-        }
-        np = c->np_pj;
+        CHK(res_step(c, j, rp, slot(c, s0), np, slot(c, s1), nullptr, gk::RES_HH_UP, c->w));
         std::swap(s0, s1);
+        np = 1;  // slot s0[0]: the rank-summed total
+    } else {
+        // w = P_j .. P_1 w ; the last reflection also accumulates ||w(j+1:n)||^2
+        for (int i = 1; i <= j; ++i) {
+            CHK(allreduce(c, slot(c, s0), np));
+            const double *va = P + (i64)(i - 1) * ld;
+            if (i < j) {
+                CHK(proj(c, gk::PJ_AXPY_DOT, c->w, va, P + (i64)i * ld, slot(c, s0), np, slot(c, s1), nullptr,
+                         2.0));
+            } else {
+                CHK(proj(c, gk::PJ_AXPY_NORM, c->w, va, nullptr, slot(c, s0), np, slot(c, s1), nullptr, 2.0,
+                         (i64)j - c->g0));
+            }
+            np = c->np_pj;
+            std::swap(s0, s1);
+        }
+        CHK(allreduce(c, slot(c, s0), np));
     }
-    CHK(allreduce(c, slot(c, s0), np));
     CHK(hh_pivot(c, j, nullptr, 0));
     {
         ProfScope ps(c, GK_KID_OTHER);

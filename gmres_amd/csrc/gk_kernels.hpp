@@ -18,6 +18,7 @@
 // dot-product summation order differs.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 namespace gk {
 
@@ -959,7 +960,36 @@ struct ResArgs {
     XsPeers peers;        // nranks > 1: device exchange regions
     int nranks, rank;
     unsigned xseq0;       // exchange p uses sequence number xseq0 + 1 + p
+    int mode;             // RES_MGS / RES_HH_UP / RES_HH_DOWN (res_col)
+    double coef;          // AXPY coefficient: w -= (coef*h) V_i (1 for MGS, 2 for reflections)
+    i64 tail0;            // RES_HH_UP: the closing norm counts local indices >= tail0
 };
+
+// Projection sequences of a resident launch (all columns of V, stride ld):
+//  RES_MGS     gmres_mgsr.f90:341-363   2j projections i = p mod j, pre-dot from
+//              pin, closes with ||w||, V(:,j+1) = w/||w|| and H(1:j+1,j)
+//  RES_HH_UP   gmres_hh.f90:290-305     w = P_j..P_1 w: i = p (p < j), pre-dot
+//              from pin, closes with ||w(j+1:n)||^2 -> hs[0]; w back to HBM
+//  RES_HH_DOWN gmres_hh.f90:269-283     v = P_1..P_j v: i = j-1-p, the pre-dot
+//              is computed in the launch, no closing reduction; v back to HBM
+// A reflection is the projection with coef 2 (w -= 2<w,P_i> P_i).
+enum { RES_MGS = 0, RES_HH_UP = 1, RES_HH_DOWN = 2 };
+enum { RK_NONE = 0, RK_DOT = 1, RK_NORM = 2 };  // reduction closing a pass
+
+__device__ __forceinline__ int res_np(int mode, int j) { return mode == RES_MGS ? 2 * j : j; }
+__device__ __forceinline__ int res_col(int mode, int j, int p) {
+    const int np = res_np(mode, j);
+    p = p < np ? p : np - 1;
+    return mode == RES_MGS ? p % j : (mode == RES_HH_UP ? p : j - 1 - p);
+}
+
+// acc += v.x^2 + v.y^2 for the element pair of local double2 index e2 (TAIL:
+// only the elements at local index >= tail0).
+template <bool TAIL>
+__device__ __forceinline__ void sq_acc(double &acc, const double2 &v, i64 e2, i64 tail0) {
+    if (!TAIL || 2 * e2 >= tail0) acc = acc + v.x * v.x;
+    if (!TAIL || 2 * e2 + 1 >= tail0) acc = acc + v.y * v.y;
+}
 
 __device__ __forceinline__ double block_sum_rt(double v, double *sm) {
     v = wave_sum(v);
@@ -1066,7 +1096,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
 // PF: the next column is loaded into a third register array before the wait;
 // CW: wave 0 holds no data and only runs the exchange, so its polls never wait
 //     behind prefetch loads (vmcnt retires in issue order).
-template <int R2, int L2, bool PF, bool NT, bool CW>
+template <int R2, int L2, bool PF, bool NT, bool CW, int MODE>
 __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
     extern __shared__ double2 lw[];  // L2 > 0: [L2][DT] LDS-resident part of w
     __shared__ double sm[RWAVES];
@@ -1078,8 +1108,10 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
     const int t = threadIdx.x;
     const bool data = !CW || t >= 64;
     const int td = CW ? t - 64 : t;
-    const int j = a.j, np = 2 * j;
+    constexpr int mode = MODE;
+    const int j = a.j, np = res_np(mode, j);
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
+    const i64 tail0 = mode == RES_HH_UP ? a.tail0 : 0;
     // Resident layout in chunks of DT double2 (data thread td holds element td
     // of each): registers hold chunks b*R2 + k (k < R2), LDS chunks G*R2 + b*L2
     // + k (k < L2); a chunk is resident when it lies below nres2 (a multiple of
@@ -1098,44 +1130,79 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         if constexpr (PF) xb[k] = double2{0.0, 0.0};
         if (data && c0 + k < nch) {
             wr[k] = W2[(c0 + k) * DT + td];
-            xa[k] = colchunk(0, c0 + k)[td];                         // V(:,1): AXPY partner of projection 0
-            if constexpr (PF) xb[k] = colchunk(1 % j, c0 + k)[td];  // its dot partner
+            xa[k] = colchunk(res_col(mode, j, 0), c0 + k)[td];              // AXPY partner of projection 0
+            if constexpr (PF) xb[k] = colchunk(res_col(mode, j, 1), c0 + k)[td];  // its dot partner
         }
     }
     if constexpr (L2 > 0) {
         for (int k = 0; k < L2; ++k)
             if (data && l0 + k < nch) lw[k * DT + td] = W2[(l0 + k) * DT + td];
     }
+    const i64 sstride = (i64)gridDim.x * DT;
+    const i64 sbase = a.nres2 + (i64)blockIdx.x * DT + td;
+    int xi = 0;  // exchange index
     double h;
-    {
+    bool ok = true;
+    if (mode == RES_HH_DOWN) {  // the pre-dot <v, V_col(0)> (xa holds V_col(0))
+        const int q = res_col(mode, j, 0);
+        const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
+        double acc = 0.0;
+        if (data) {
+#pragma unroll
+            for (int k = 0; k < R2; ++k) {
+                acc = acc + wr[k].x * xa[k].x;
+                acc = acc + wr[k].y * xa[k].y;
+            }
+            if constexpr (L2 > 0) {
+                for (int k = 0; k < L2; ++k)
+                    if (l0 + k < nch) {
+                        const double2 wv = lw[k * DT + td], bv = ldv<NT>(B2 + (l0 + k) * DT + td);
+                        acc = acc + wv.x * bv.x;
+                        acc = acc + wv.y * bv.y;
+                    }
+            }
+            for (i64 e = sbase; e < n2; e += sstride) {
+                const double2 wv = W2[e], bv = ldv<NT>(B2 + e);
+                acc = acc + wv.x * bv.x;
+                acc = acc + wv.y * bv.y;
+            }
+            if ((a.n & 1) && blockIdx.x == 0 && td == 0) acc = acc + a.w[a.n - 1] * a.V[(i64)q * a.ld + a.n - 1];
+        }
+        acc = wave_sum(acc);
+        if ((t & 63) == 0) sm[t >> 6] = acc;
+        __syncthreads();
+        if (t < 64) res_exchange(a, xi, sm, bc, &okf);
+        __syncthreads();
+        ++xi;
+        h = bc[0];
+        ok = okf != 0;
+    } else {
         double s = 0.0;
         for (int k = t; k < a.npin; k += RT) s += a.pin[k];
         h = block_sum_rt(s, sm);
     }
-    const i64 sstride = (i64)gridDim.x * DT;
-    const i64 sbase = a.nres2 + (i64)blockIdx.x * DT + td;
     // Projection p: i = p mod j, AXPY w -= h V_i (h = the dot of p), then the
     // dot of projection p+1 with V_q, q = (p+1) mod j -- or ||w||^2 after the
     // last one.  X holds V_i; PF: Y holds V_q (prefetched), and X <- the dot
     // partner of p+1 is loaded before the wait.
     auto proj = [&](int p, auto &X, auto &Y) -> bool {
-        const int i = p % j;
+        const int i = res_col(mode, j, p);
         const bool last = p == np - 1;
-        const int q = last ? i : (p + 1) % j;
-        if (blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
+        const int q = res_col(mode, j, p + 1);
+        const int kind = !last ? RK_DOT : (mode == RES_HH_DOWN ? RK_NONE : RK_NORM);
+        if (mode == RES_MGS && blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
+        const double ch = mode == RES_MGS ? h : a.coef * h;
         double acc = 0.0;
         if (data) {
 #pragma unroll
             for (int k = 0; k < R2; ++k) {
-                wr[k].x = wr[k].x - h * X[k].x;
-                wr[k].y = wr[k].y - h * X[k].y;
+                wr[k].x = wr[k].x - ch * X[k].x;
+                wr[k].y = wr[k].y - ch * X[k].y;
             }
-            if (last) {
+            if (kind == RK_NONE) {
+            } else if (last) {
 #pragma unroll
-                for (int k = 0; k < R2; ++k) {
-                    acc = acc + wr[k].x * wr[k].x;
-                    acc = acc + wr[k].y * wr[k].y;
-                }
+                for (int k = 0; k < R2; ++k) sq_acc<mode == RES_HH_UP>(acc, wr[k], (c0 + k) * DT + td, tail0);
             } else if constexpr (PF) {
 #pragma unroll
                 for (int k = 0; k < R2; ++k) {
@@ -1170,12 +1237,12 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                     for (int u = 0; u < 2; ++u) {
                         const i64 c = l0 + k + u;
                         if (k + u < L2 && c < nch) {
-                            wv[u].x = wv[u].x - h * av[u].x;
-                            wv[u].y = wv[u].y - h * av[u].y;
+                            wv[u].x = wv[u].x - ch * av[u].x;
+                            wv[u].y = wv[u].y - ch * av[u].y;
                             lw[(k + u) * DT + td] = wv[u];
-                            if (last) {
-                                acc = acc + wv[u].x * wv[u].x;
-                                acc = acc + wv[u].y * wv[u].y;
+                            if (kind == RK_NONE) {
+                            } else if (last) {
+                                sq_acc<mode == RES_HH_UP>(acc, wv[u], c * DT + td, tail0);
                             } else {
                                 acc = acc + wv[u].x * bv[u].x;
                                 acc = acc + wv[u].y * bv[u].y;
@@ -1199,12 +1266,12 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                 for (int u = 0; u < 2; ++u) {
                     const i64 e = e0 + u * sstride;
                     if (e < n2) {
-                        wv[u].x = wv[u].x - h * av[u].x;
-                        wv[u].y = wv[u].y - h * av[u].y;
+                        wv[u].x = wv[u].x - ch * av[u].x;
+                        wv[u].y = wv[u].y - ch * av[u].y;
                         W2[e] = wv[u];
-                        if (last) {
-                            acc = acc + wv[u].x * wv[u].x;
-                            acc = acc + wv[u].y * wv[u].y;
+                        if (kind == RK_NONE) {
+                        } else if (last) {
+                            sq_acc<mode == RES_HH_UP>(acc, wv[u], e, tail0);
                         } else {
                             acc = acc + wv[u].x * bv[u].x;
                             acc = acc + wv[u].y * bv[u].y;
@@ -1214,28 +1281,30 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
             }
             if ((a.n & 1) && blockIdx.x == 0 && td == 0) {  // odd-length tail element
                 const i64 e = a.n - 1;
-                const double x = a.w[e] - h * a.V[(i64)i * a.ld + e];
+                const double x = a.w[e] - ch * a.V[(i64)i * a.ld + e];
                 a.w[e] = x;
-                acc = acc + (last ? x * x : x * a.V[(i64)q * a.ld + e]);
+                if (kind == RK_DOT) acc = acc + x * a.V[(i64)q * a.ld + e];
+                if (kind == RK_NORM && e >= tail0) acc = acc + x * x;
             }
         }
+        if (kind == RK_NONE) return true;
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
         if constexpr (PF) {
             if (data && p + 2 < np) {  // the dot partner of projection p+1, in flight during the exchange
-                const int q2 = (p + 2) % j;
+                const int q2 = res_col(mode, j, p + 2);
 #pragma unroll
                 for (int k = 0; k < R2; ++k)
                     if (c0 + k < nch) X[k] = ldv<NT>(colchunk(q2, c0 + k) + td);
             }
         }
-        if (t < 64) res_exchange(a, p, sm, bc, &okf);
+        if (t < 64) res_exchange(a, xi, sm, bc, &okf);
         __syncthreads();
+        ++xi;
         h = bc[0];
         return okf != 0;
     };
-    bool ok = true;
     if constexpr (PF) {
         for (int p = 0; p < np && ok; p += 2) {
             ok = proj(p, xa, xb);
@@ -1245,6 +1314,19 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         for (int p = 0; p < np && ok; ++p) ok = proj(p, xa, xb);
     }
     if (!ok) return;  // uniform per workgroup; *err is set
+    if (mode != RES_MGS) {  // reflections: the resident part of w back to HBM
+        if (data) {
+#pragma unroll
+            for (int k = 0; k < R2; ++k)
+                if (c0 + k < nch) W2[(c0 + k) * DT + td] = wr[k];
+            if constexpr (L2 > 0) {
+                for (int k = 0; k < L2; ++k)
+                    if (l0 + k < nch) W2[(l0 + k) * DT + td] = lw[k * DT + td];
+            }
+        }
+        if (mode == RES_HH_UP && blockIdx.x == 0 && t == 0) a.hs[0] = h;  // ||w(j+1:n)||^2
+        return;
+    }
     // h = ||w|| ; V(:,j+1) = w / h  (h == 0: zeros, as k_scale)
     const double hn = sqrt(h);
     double2 *__restrict__ O2 = reinterpret_cast<double2 *>(a.vout);
@@ -1292,7 +1374,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
 constexpr int WT = 256;  // threads per workgroup (4 waves, one per SIMD)
 constexpr int WB = 8;    // double2 per column per batch in flight per thread
 
-template <int RW, int LW>
+template <int RW, int LW, int MODE>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     extern __shared__ double2 lw[];  // [LW][WT]
     __shared__ double sm[WT / 64];
@@ -1300,11 +1382,13 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     __shared__ int okf;
     __shared__ double hsh[RHMAX + 1];
     const int t = threadIdx.x;
-    const int j = a.j, np = 2 * j;
+    constexpr int mode = MODE;
+    const int j = a.j, np = res_np(mode, j);
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
     const i64 nch = a.nres2 / WT;
     const i64 c0 = (i64)blockIdx.x * RW;
     const i64 l0 = (i64)gridDim.x * RW + (i64)blockIdx.x * LW;
+    const i64 tail0 = mode == RES_HH_UP ? a.tail0 : 0;
     const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
     double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
     double2 wr[RW];
@@ -1312,28 +1396,23 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < nch) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
     for (int k = 0; k < LW; ++k)
         if (l0 + k < nch) lw[k * WT + t] = W2[(l0 + k) * WT + t];
-    double h;
-    {
-        double s = 0.0;
-        for (int k = t; k < a.npin; k += WT) s += a.pin[k];
-        s = wave_sum(s);
-        if ((t & 63) == 0) sm[t >> 6] = s;
-        __syncthreads();
-        h = sm[0];
-#pragma unroll
-        for (int w = 1; w < WT / 64; ++w) h += sm[w];
-        __syncthreads();
-    }
     const i64 sstride = (i64)gridDim.x * WT;
     const i64 sbase = a.nres2 + (i64)blockIdx.x * WT + t;
-    bool ok = true;
-    for (int p = 0; p < np && ok; ++p) {
-        const int i = p % j;
-        const bool last = p == np - 1;
-        const int q = last ? i : (p + 1) % j;
-        if (blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
+    // acc += the closing reduction of element pair e2 (local double2 index)
+    auto red = [&](double &acc, const double2 &v, const double2 &b, int kind, i64 e2) {
+        if (kind == RK_DOT) {
+            acc = acc + v.x * b.x;
+            acc = acc + v.y * b.y;
+        } else if (kind == RK_NORM) {
+            sq_acc<mode == RES_HH_UP>(acc, v, e2, tail0);
+        }
+    };
+    // One pass over the slab: w -= ch V_i, then the reduction `kind`
+    // (<w, V_q>, ||w(tail0:)||^2, or none).  Returns this thread's partial.
+    auto pass = [&](double ch, int i, int q, int kind) -> double {
         const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
         const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
+        const bool dot = kind == RK_DOT;
         double acc = 0.0;
         // registers: batches of WB chunks, both columns in flight
 #pragma unroll
@@ -1344,22 +1423,16 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 const i64 c = c0 + k0 + u;
                 if (k0 + u < RW && c < nch) {
                     av[u] = ldv<true>(A2 + c * WT + t);
-                    if (!last) bv[u] = B2[c * WT + t];
+                    if (dot) bv[u] = B2[c * WT + t];
                 }
             }
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
                 const int k = k0 + u;
                 if (k < RW && c0 + k < nch) {
-                    wr[k].x = wr[k].x - h * av[u].x;
-                    wr[k].y = wr[k].y - h * av[u].y;
-                    if (last) {
-                        acc = acc + wr[k].x * wr[k].x;
-                        acc = acc + wr[k].y * wr[k].y;
-                    } else {
-                        acc = acc + wr[k].x * bv[u].x;
-                        acc = acc + wr[k].y * bv[u].y;
-                    }
+                    wr[k].x = wr[k].x - ch * av[u].x;
+                    wr[k].y = wr[k].y - ch * av[u].y;
+                    red(acc, wr[k], bv[u], kind, (c0 + k) * WT + t);
                 }
             }
         }
@@ -1371,7 +1444,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 const i64 c = l0 + k0 + u;
                 if (k0 + u < LW && c < nch) {
                     av[u] = ldv<true>(A2 + c * WT + t);
-                    if (!last) bv[u] = B2[c * WT + t];
+                    if (dot) bv[u] = B2[c * WT + t];
                 }
             }
 #pragma unroll
@@ -1379,16 +1452,10 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 const int k = k0 + u;
                 if (k < LW && l0 + k < nch) {
                     double2 wv = lw[k * WT + t];
-                    wv.x = wv.x - h * av[u].x;
-                    wv.y = wv.y - h * av[u].y;
+                    wv.x = wv.x - ch * av[u].x;
+                    wv.y = wv.y - ch * av[u].y;
                     lw[k * WT + t] = wv;
-                    if (last) {
-                        acc = acc + wv.x * wv.x;
-                        acc = acc + wv.y * wv.y;
-                    } else {
-                        acc = acc + wv.x * bv[u].x;
-                        acc = acc + wv.y * bv[u].y;
-                    }
+                    red(acc, wv, bv[u], kind, (l0 + k) * WT + t);
                 }
             }
         }
@@ -1400,41 +1467,77 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 if (e < n2) {
                     wv[u] = W2[e];
                     av[u] = ldv<true>(A2 + e);
-                    if (!last) bv[u] = B2[e];
+                    if (dot) bv[u] = B2[e];
                 }
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const i64 e = e0 + u * sstride;
                 if (e < n2) {
-                    wv[u].x = wv[u].x - h * av[u].x;
-                    wv[u].y = wv[u].y - h * av[u].y;
+                    wv[u].x = wv[u].x - ch * av[u].x;
+                    wv[u].y = wv[u].y - ch * av[u].y;
                     W2[e] = wv[u];
-                    if (last) {
-                        acc = acc + wv[u].x * wv[u].x;
-                        acc = acc + wv[u].y * wv[u].y;
-                    } else {
-                        acc = acc + wv[u].x * bv[u].x;
-                        acc = acc + wv[u].y * bv[u].y;
-                    }
+                    red(acc, wv[u], bv[u], kind, e);
                 }
             }
         }
         if ((a.n & 1) && blockIdx.x == 0 && t == 0) {  // odd-length tail element
             const i64 e = a.n - 1;
-            const double x = a.w[e] - h * a.V[(i64)i * a.ld + e];
+            const double x = a.w[e] - ch * a.V[(i64)i * a.ld + e];
             a.w[e] = x;
-            acc = acc + (last ? x * x : x * a.V[(i64)q * a.ld + e]);
+            if (kind == RK_DOT) acc = acc + x * a.V[(i64)q * a.ld + e];
+            if (kind == RK_NORM && e >= tail0) acc = acc + x * x;
         }
+        return acc;
+    };
+    // all-gather of the partials: the same h in every workgroup (and rank)
+    int xi = 0;
+    auto reduce = [&](double acc, double &h) -> bool {
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
-        if (t < 64) res_exchange<WT / 64>(a, p, sm, bc, &okf);
+        if (t < 64) res_exchange<WT / 64>(a, xi, sm, bc, &okf);
         __syncthreads();
+        ++xi;
         h = bc[0];
-        ok = okf != 0;
+        return okf != 0;
+    };
+    double h;
+    bool ok = true;
+    if (mode == RES_HH_DOWN) {
+        // the pre-dot as an AXPY pass with h = 0 (w - 0 V = w): a dot-only copy of the
+        // unrolled register loop would not fit the register file
+        const int q = res_col(mode, j, 0);
+        ok = reduce(pass(0.0, q, q, RK_DOT), h);
+    } else {
+        double s = 0.0;
+        for (int k = t; k < a.npin; k += WT) s += a.pin[k];
+        s = wave_sum(s);
+        if ((t & 63) == 0) sm[t >> 6] = s;
+        __syncthreads();
+        h = sm[0];
+#pragma unroll
+        for (int w = 1; w < WT / 64; ++w) h += sm[w];
+        __syncthreads();
+    }
+    for (int p = 0; p < np && ok; ++p) {
+        const int i = res_col(mode, j, p);
+        const bool last = p == np - 1;
+        const int kind = !last ? RK_DOT : (mode == RES_HH_DOWN ? RK_NONE : RK_NORM);
+        if (mode == RES_MGS && blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
+        const double acc = pass(mode == RES_MGS ? h : a.coef * h, i, res_col(mode, j, p + 1), kind);
+        if (kind != RK_NONE) ok = reduce(acc, h);
     }
     if (!ok) return;  // uniform per workgroup; *err is set
+    if (mode != RES_MGS) {  // reflections: the resident part of w back to HBM
+#pragma unroll
+        for (int k = 0; k < RW; ++k)
+            if (c0 + k < nch) W2[(c0 + k) * WT + t] = wr[k];
+        for (int k = 0; k < LW; ++k)
+            if (l0 + k < nch) W2[(l0 + k) * WT + t] = lw[k * WT + t];
+        if (mode == RES_HH_UP && blockIdx.x == 0 && t == 0) a.hs[0] = h;  // ||w(j+1:n)||^2
+        return;
+    }
     const double hn = sqrt(h);
     double2 *__restrict__ O2 = reinterpret_cast<double2 *>(a.vout);
 #pragma unroll

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 T_RES, T_R2, T_SHARE, T_TMO = 8, 9, 10, 11
 
 
-def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False, wonly=-1):
+def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False, wonly=-1, method="mgsr"):
     import gmres_amd as ga
 
     with ga.Context(N, m) as c:
@@ -33,7 +33,10 @@ def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False, wo
         if want_prof:
             c.profile(True)
             c.profile_reset()
-        r = ga.gmres_mgsr(c, 1e-15, max_cycles=cycles, want_hist=True)
+        if method == "hh":
+            r = ga.gmres_hh(c, 1e-15, precondition=(prec != "identity"), max_cycles=cycles, want_hist=True)
+        else:
+            r = ga.gmres_mgsr(c, 1e-15, max_cycles=cycles, want_hist=True)
         prof = c.profile_read() if want_prof else None
     return r, prof
 
@@ -101,3 +104,43 @@ def test_resident_1024_vs_reference():
     got, prof = _run(1024, 95, "identity", res=1, cycles=3, want_prof=True)
     assert prof["res"][1] > 0
     assert np.allclose(got.hist_res, g[: len(got.hist_res)], rtol=1e-9, atol=0.0)
+
+
+# Householder steps as resident reflection chains (gk::RES_HH_DOWN: v_j = P_1..P_j e_j,
+# gmres_hh.f90:269-283; gk::RES_HH_UP: w = P_j..P_1 A v_j + ||w(j+1:n)||^2, :290-305), in
+# every variant of the resident kernels.  The reflection arithmetic is k_proj's with
+# coef 2 (bit-identical element-wise); only the dot summation order differs.
+HCASES = [
+    # N, m, prec, r2 cap, share, w-only
+    (64, 20, "identity", 0, 1, -1),     # fully resident, R2 = 2, prefetch
+    (45, 12, "cbpr2", 2, 64, -1),       # odd N (tail element), streamed part
+    (200, 25, "identity", 4, 32, -1),   # R2 = 4 with a streamed part
+    (256, 40, "identity", 12, 16, -1),  # two-array variant + LDS-resident w
+    (300, 20, "identity", 12, 64, 1),   # w-only: registers + LDS + streamed
+    (181, 16, "cbpr2", 12, 128, 1),     # w-only, odd N
+]
+
+
+@pytest.mark.parametrize("N,m,prec,r2,share,wonly", HCASES)
+def test_resident_householder_matches_launch_path(N, m, prec, r2, share, wonly):
+    ref, _ = _run(N, m, prec, res=0, method="hh")
+    got, prof = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True, wonly=wonly, method="hh")
+    assert prof["res"][1] > 0 and prof["proj"][1] < prof["res"][1] // 4, prof  # k_proj: diagnostics only
+    assert got.n_cycles == ref.n_cycles
+    h, r = got.hist_res, ref.hist_res
+    tol = np.where(r > 1e-6, 1e-9, np.where(r > 1e-12, 1e-3, 5e-2))  # HH tiers (test_gpu_solver)
+    assert np.all(np.abs(h - r) <= tol * r + 1e-16), (h, r)
+
+
+def test_resident_householder_vs_oracle_to_convergence(oracle):
+    """Config 1 shape, gmres_hh_omp (full cycles) on the resident path, against the
+    oracle with the Householder tiers of test_gpu_solver._hist_close_hh."""
+    got, prof = _run(128, 30, "identity", res=1, cycles=1000, want_prof=True, method="hh")
+    ref = oracle.gmres_hh(oracle.rhs_ones(128), 128, 30, midcycle_exit=0)
+    assert prof["res"][1] > 0
+    assert got.iterations == ref.iterations
+    k = min(len(got.hist_res), len(ref.hist_res))
+    g, r = got.hist_res[:k], ref.hist_res[:k]
+    rtol = np.where(r > 1e-6, 1e-8, np.where(r > 1e-12, 1e-3, 5e-2))
+    assert np.all(np.abs(g - r) <= rtol * r + 1e-16)
+    assert np.max(np.abs(got.x - 1.0)) < 1e-9
