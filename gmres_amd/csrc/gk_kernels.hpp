@@ -983,12 +983,19 @@ __device__ __forceinline__ int res_col(int mode, int j, int p) {
     return mode == RES_MGS ? p % j : (mode == RES_HH_UP ? p : j - 1 - p);
 }
 
-// acc += v.x^2 + v.y^2 for the element pair of local double2 index e2 (TAIL:
-// only the elements at local index >= tail0).
-template <bool TAIL>
-__device__ __forceinline__ void sq_acc(double &acc, const double2 &v, i64 e2, i64 tail0) {
-    if (!TAIL || 2 * e2 >= tail0) acc = acc + v.x * v.x;
-    if (!TAIL || 2 * e2 + 1 >= tail0) acc = acc + v.y * v.y;
+// acc += v.x^2 + v.y^2 for the element pair of local double2 index e2; with chk
+// only the elements at local index >= tail0.  tail0 <= j <= RHMAX lies inside the
+// first chunk of the vector, so callers pass a uniform chk that is true for that
+// chunk only (RES_HH_UP): the per-element test stays out of every other chunk,
+// and out of the register allocation of the steady-state loop.
+__device__ __forceinline__ void sq_acc(double &acc, const double2 &v, i64 e2, i64 tail0, bool chk) {
+    if (chk) {
+        if (2 * e2 >= tail0) acc = acc + v.x * v.x;
+        if (2 * e2 + 1 >= tail0) acc = acc + v.y * v.y;
+    } else {
+        acc = acc + v.x * v.x;
+        acc = acc + v.y * v.y;
+    }
 }
 
 __device__ __forceinline__ double block_sum_rt(double v, double *sm) {
@@ -1202,7 +1209,8 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
             if (kind == RK_NONE) {
             } else if (last) {
 #pragma unroll
-                for (int k = 0; k < R2; ++k) sq_acc<mode == RES_HH_UP>(acc, wr[k], (c0 + k) * DT + td, tail0);
+                for (int k = 0; k < R2; ++k)
+                    sq_acc(acc, wr[k], (c0 + k) * DT + td, tail0, mode == RES_HH_UP && c0 + k == 0);
             } else if constexpr (PF) {
 #pragma unroll
                 for (int k = 0; k < R2; ++k) {
@@ -1242,7 +1250,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                             lw[(k + u) * DT + td] = wv[u];
                             if (kind == RK_NONE) {
                             } else if (last) {
-                                sq_acc<mode == RES_HH_UP>(acc, wv[u], c * DT + td, tail0);
+                                sq_acc(acc, wv[u], c * DT + td, tail0, mode == RES_HH_UP && c == 0);
                             } else {
                                 acc = acc + wv[u].x * bv[u].x;
                                 acc = acc + wv[u].y * bv[u].y;
@@ -1271,7 +1279,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                         W2[e] = wv[u];
                         if (kind == RK_NONE) {
                         } else if (last) {
-                            sq_acc<mode == RES_HH_UP>(acc, wv[u], e, tail0);
+                            sq_acc(acc, wv[u], e, tail0, mode == RES_HH_UP && 2 * a.nres2 < tail0);
                         } else {
                             acc = acc + wv[u].x * bv[u].x;
                             acc = acc + wv[u].y * bv[u].y;
@@ -1399,12 +1407,12 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     const i64 sstride = (i64)gridDim.x * WT;
     const i64 sbase = a.nres2 + (i64)blockIdx.x * WT + t;
     // acc += the closing reduction of element pair e2 (local double2 index)
-    auto red = [&](double &acc, const double2 &v, const double2 &b, int kind, i64 e2) {
+    auto red = [&](double &acc, const double2 &v, const double2 &b, int kind, i64 e2, bool chk) {
         if (kind == RK_DOT) {
             acc = acc + v.x * b.x;
             acc = acc + v.y * b.y;
         } else if (kind == RK_NORM) {
-            sq_acc<mode == RES_HH_UP>(acc, v, e2, tail0);
+            sq_acc(acc, v, e2, tail0, chk);
         }
     };
     // One pass over the slab: w -= ch V_i, then the reduction `kind`
@@ -1432,7 +1440,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 if (k < RW && c0 + k < nch) {
                     wr[k].x = wr[k].x - ch * av[u].x;
                     wr[k].y = wr[k].y - ch * av[u].y;
-                    red(acc, wr[k], bv[u], kind, (c0 + k) * WT + t);
+                    red(acc, wr[k], bv[u], kind, (c0 + k) * WT + t, mode == RES_HH_UP && c0 + k == 0);
                 }
             }
         }
@@ -1455,7 +1463,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                     wv.x = wv.x - ch * av[u].x;
                     wv.y = wv.y - ch * av[u].y;
                     lw[k * WT + t] = wv;
-                    red(acc, wv, bv[u], kind, (l0 + k) * WT + t);
+                    red(acc, wv, bv[u], kind, (l0 + k) * WT + t, mode == RES_HH_UP && l0 + k == 0);
                 }
             }
         }
@@ -1477,7 +1485,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                     wv[u].x = wv[u].x - ch * av[u].x;
                     wv[u].y = wv[u].y - ch * av[u].y;
                     W2[e] = wv[u];
-                    red(acc, wv[u], bv[u], kind, e);
+                    red(acc, wv[u], bv[u], kind, e, mode == RES_HH_UP && 2 * a.nres2 < tail0);
                 }
             }
         }
