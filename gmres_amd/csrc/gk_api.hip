@@ -569,7 +569,10 @@ constexpr int RES_LDS_MIN = 96 * 1024;  // dynamic LDS: > half a CU's 160 KiB, s
 constexpr int RES_L2 = 18;              // LDS-resident double2 of w per data thread (18 x 512 x 16 B = 144 KiB)
 constexpr int RES_R2_BIG = 12;          // two register arrays of 12 double2 fit 256 VGPRs without spills
 
-constexpr int RES_RW = 64, RES_LW = 38;  // w-only variant: double2 of w per thread in registers / LDS
+#ifndef GK_RES_RW
+#define GK_RES_RW 88
+#endif
+constexpr int RES_RW = GK_RES_RW, RES_LW = 38;  // w-only variant: double2 of w per thread in registers / LDS
 
 struct ResPlan {
     int G = 0, r2 = 0, l2 = 0;
