@@ -128,13 +128,14 @@ def test_slabs_match_single_context(nranks, method, prec, degree):
     _check_against_single(ref, res, method)
 
 
-@pytest.mark.parametrize("prec,degree", [("identity", 1), ("cbpr2", 1), ("cheb", 4)])
-def test_resident_step_over_device_exchange(prec, degree):
-    """Resident MGS-R step (one persistent launch per Arnoldi step) with the rank
+@pytest.mark.parametrize("method,prec,degree", [("mgsr", "identity", 1), ("mgsr", "cbpr2", 1), ("mgsr", "cheb", 4),
+                                                ("hh", "identity", 1), ("hh", "cbpr2", 1)])
+def test_resident_step_over_device_exchange(method, prec, degree):
+    """Resident launches (MGS-R step; Householder reflection chains) with the rank
     totals exchanged inside the launch: two ranks on one GPU, forced on
     (GK_TUNE_RES = 1; auto mode keeps it off when contexts share a device)."""
     N, m, cyc = 66, 16, 6
-    ref = _single(N, m, "mgsr", prec, degree, cyc)
+    ref = _single(N, m, method, prec, degree, cyc)
     g, ctxs = _local_group(N, m, 2)
     for c in ctxs:
         c.tune(8, 1)
@@ -146,14 +147,14 @@ def test_resident_step_over_device_exchange(prec, degree):
         c.set_rhs_ones()
         c.profile(True)
         c.profile_reset()
-        out = _solve(c, "mgsr", prec, cyc)
+        out = _solve(c, method, prec, cyc)
         return out, c.profile_read()
 
     out = _run_threads(2, work)
     _close(g, ctxs)
     res = [o[0] for o in out]
     assert all(o[1]["res"][1] > 0 for o in out)
-    _check_against_single(ref, res, "mgsr")
+    _check_against_single(ref, res, method)
 
 
 def test_lanczos_and_verr_over_device_exchange():
