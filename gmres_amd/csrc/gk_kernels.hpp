@@ -487,6 +487,9 @@ __global__ __launch_bounds__(TPB) void k_stencil(StArgs a) {
             double in1v[VEC], in2v[VEC];
             if (OP == OP_RESID || OP == OP_CHEB_ITER) ld_vec<VEC>(a.in1 + row + i0, act, in1v);
             if (OP == OP_CHEB_ITER) ld_vec<VEC>(a.in2 + row + i0, act, in2v);
+            // the dot operand is issued with the line loads, not after the store
+            double vd[VEC];
+            if (ACC == ACC_DOT) ld_vec<VEC>(a.vdot + row + i0, act, vd);
             double resv[VEC], dnv[VEC];
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
@@ -522,8 +525,6 @@ __global__ __launch_bounds__(TPB) void k_stencil(StArgs a) {
                     if (a.o_d != nullptr) st_vec<VEC>(a.o_d + row + i0, dnv);
                 }
                 if (ACC == ACC_DOT) {
-                    double vd[VEC];
-                    ld_vec<VEC>(a.vdot + row + i0, true, vd);
 #pragma unroll
                     for (int k = 0; k < VEC; ++k) acc = acc + yv[k] * vd[k];
                 } else if (ACC == ACC_NORM) {
