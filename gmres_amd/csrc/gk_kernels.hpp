@@ -468,11 +468,15 @@ __global__ __launch_bounds__(TPB) void k_stencil(StArgs a) {
     };
 
     if (j0 < a.nlines) {
-        double rm[VEC], rc[VEC], rp[VEC], tm[VEC], tc[VEC], tp[VEC];
+        // lines j-1, j, j+1 in registers and line j+2 in flight while line j is computed
+        double rm[VEC], rc[VEC], rp[VEC], tm[VEC], tc[VEC], tp[VEC], rn[VEC], tn[VEC];
         load_line(j0 - 1, rm, tm);
         load_line(j0, rc, tc);
+        load_line(j0 + 1, rp, tp);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) rn[k] = tn[k] = 0.0;
         for (int j = j0; j < j1; ++j) {
-            load_line(j + 1, rp, tp);
+            if (j + 2 <= j1) load_line(j + 2, rn, tn);
             const i64 row = (i64)j * N;
             // W/E neighbours of the lane's first / last point
             double left = __shfl_up(tc[VEC - 1], 1, 64);  // previous lane's last point
@@ -538,6 +542,8 @@ __global__ __launch_bounds__(TPB) void k_stencil(StArgs a) {
                 tm[k] = tc[k];
                 rc[k] = rp[k];
                 tc[k] = tp[k];
+                rp[k] = rn[k];
+                tp[k] = tn[k];
             }
         }
     }
