@@ -674,23 +674,35 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
             v[1] = t.y;
         }
     };
+    // input line t+1 is in flight while line t runs through the levels
+    auto ld_in = [&](int row, double (&d)[2], double (&r)[2], double (&z)[2]) {
+        ld2(a.din, row, d);
+        if (!FIRST) {
+            ld2(a.rin, row, r);
+            ld2(a.zin, row, z);
+        }
+    };
     if (j0 < a.nlines) {
+        double nd[2], nr[2] = {0.0, 0.0}, nz[2] = {0.0, 0.0};
+        ld_in(j0 - L - 1, nd, nr, nz);
         for (int t = j0 - L - 1; t < j1 + L; ++t) {
             // emission of "level -1": the input line t
             double ed[2], er[2], ez[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                ed[k] = nd[k];
+                er[k] = nr[k];
+                ez[k] = nz[k];
+            }
+            if (t + 1 < j1 + L) ld_in(t + 1, nd, nr, nz);
             if (FIRST) {
-                double raw[2];
-                ld2(a.din, t, raw);
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
-                    ed[k] = raw[k] / a.theta;
-                    er[k] = raw[k];
+                    const double raw = ed[k];
+                    ed[k] = raw / a.theta;
+                    er[k] = raw;
                     ez[k] = ed[k];
                 }
-            } else {
-                ld2(a.din, t, ed);
-                ld2(a.rin, t, er);
-                ld2(a.zin, t, ez);
             }
             int row = t;  // row of the current emission
 #pragma unroll
