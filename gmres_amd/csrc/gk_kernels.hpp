@@ -695,6 +695,10 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
                 ez[k] = nz[k];
             }
             if (t + 1 < j1 + L) ld_in(t + 1, nd, nr, nz);
+            // the dot partner of the line the last level emits this step (row t - L)
+            double2 vd = double2{0.0, 0.0};
+            if (LAST && ACC == ACC_DOT && t - L >= j0 && t - L < j1 && kept)
+                vd = *reinterpret_cast<const double2 *>(a.vdot + (i64)(t - L) * N + i0);
             if (FIRST) {
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
@@ -745,9 +749,8 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
                 if (LAST) {
                     *reinterpret_cast<double2 *>(a.out + idx) = double2{ez[0], ez[1]};
                     if (ACC == ACC_DOT) {
-                        const double2 v = *reinterpret_cast<const double2 *>(a.vdot + idx);
-                        acc = acc + ez[0] * v.x;
-                        acc = acc + ez[1] * v.y;
+                        acc = acc + ez[0] * vd.x;
+                        acc = acc + ez[1] * vd.y;
                     } else if (ACC == ACC_NORM) {
                         acc = acc + ez[0] * ez[0];
                         acc = acc + ez[1] * ez[1];
