@@ -546,7 +546,7 @@ void or_pcg(const double *b, int N, double tol, int *iter, double *res_out, int 
             int degree, double *x, double *hist_res) {
     const i64 n = (i64)N * N;
     double *ax = (double *)malloc(sizeof(double) * n), *p = (double *)malloc(sizeof(double) * n);
-    double *r = (double *)malloc(sizeof(double) * n), *z = (double *)malloc(sizeof(double) * n);
+    double *r = (double *)calloc((size_t)n, sizeof(double)), *z = (double *)malloc(sizeof(double) * n);
     double *aux = (double *)malloc(sizeof(double) * n), *aux2 = (double *)malloc(sizeof(double) * n);
     int maxit = *iter, converged = 0;
     double res = 0.0;
