@@ -9,13 +9,18 @@ a solve does; K timed steps are K consecutive cycles of one solve.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 4096] [--m 95]
                   [--prec identity|cbpr2|cheb] [--method mgsr|hh] [--no-cpu]
+                  [--plan-only]
 
-N > 1 is launched by torch.distributed.run (one rank per GPU): the grid is
-split into row-block slabs of grid lines; dot-product slabs are RCCL
-all-reduced and halo lines exchanged inside libgmres_hip (one RCCL
-communicator owned by the C-ABI context); torch.distributed (gloo) is used only
-for bootstrapping the RCCL id, the barriers and the max-over-ranks timing.
-Scaling is strong: the global grid is fixed as N grows.
+--gpus N > 1: one rank per GPU.  Launched under torch.distributed.run (the
+driver's way) the ranks read RANK/LOCAL_RANK/WORLD_SIZE; launched directly
+(WORLD_SIZE unset) bench.py starts torch.distributed.run itself as a child
+process -- before anything touches a GPU -- and exits with its status; it
+refuses (exit 2) when fewer than N GPUs are visible.  --plan-only prints that
+launch plan as JSON and exits.  The grid is split into row-block slabs of grid
+lines (strong scaling: the global grid is fixed as N grows); per projection
+the dot products are all-reduced inside libgmres_hip (device exchange over
+xGMI, or RCCL), halo lines exchanged point to point; torch.distributed (gloo)
+only bootstraps the communicator and times max-over-ranks.
 
 Rank 0 prints ONE JSON line.
 """
@@ -24,6 +29,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,75 +39,190 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; ~6.3 TB/s achievable)
 METRIC = "Arnoldi iters/sec + HBM GB/s, 4096² Poisson-2D fp64, GMRES(m=95)"
 
 
-def alg_bytes_cycle(n: int, m: int, prec: str, degree: int, steps: int | None = None) -> float:
-    """SURVEY 8(d) byte model: the reference's op sequence as written, every
-    vector operand read once and every result written once (fp64).
-    per MGS-R step j: (40 + 80 j) n  [stencil 16n + 2j (dot 16n + AXPY 24n) + norm 8n + scale 16n];
-    cycle start: (16 + 24 + 8 + 16) n; x update: 8 (m + 2) n;
-    cbpr2 as written: +64 n per application; Chebyshev(k): 48 n per sweep
-    (read d, r, z; write r, d, z) + 16 n stencil on entry, counted the same way."""
-    s = m if steps is None else steps
-    b = sum(40 + 80 * j for j in range(1, s + 1)) * n
-    b += 64 * n + 8 * (m + 2) * n
+# ------------------------------------------------------------- byte models ---
+# Two models per launch / per cycle:
+#  * as written: the reference's op sequence, every BLAS-1 op
+#    reading its operands and writing its result once -- dot 16n, AXPY 24n,
+#    norm 8n, scale 16n.  A fused kernel beats it, so its "fraction" can
+#    exceed 1: reported as alg_as_written_*, never as roofline.frac.
+#  * fused minimum: what the fused schedule must move at least with w held on
+#    chip -- per MGS projection (AXPY_i fused with dot_{i+1}) the two Krylov
+#    columns it touches, 16n; per resident step launch (32j + 16) n (2j
+#    projections + reading w once + writing V(:,j+1)).  roofline.frac uses it.
+
+def mgs_step_bytes(n: int, j: int, model: str) -> float:
+    """One resident MGS-R step launch (cascade + norm + scale; the stencil is
+    its own launch)."""
+    return float((80 * j + 24) * n if model == "as_written" else (32 * j + 16) * n)
+
+
+def hh_chain_bytes(n: int, L: int, model: str) -> float:
+    """One resident Householder chain of L reflections w -= 2<w,P_i>P_i."""
+    return float(40 * L * n if model == "as_written" else (16 * L + 16) * n)
+
+
+def prec_bytes(n: int, prec: str, degree: int, model: str) -> float:
+    """One preconditioner application after the stencil (z = A v already made)."""
+    if prec == "identity":
+        return 0.0
     if prec == "cbpr2":
-        b += 64 * n * (s + 1)
-    elif prec == "cheb":
-        b += (16 + 48 * degree) * n * (s + 1)
-    return float(b)
+        return float(64 * n if model == "as_written" else 16 * n)
+    # Chebyshev(k): 48n per sweep as written; the temporal-blocked passes read
+    # (d, r, z) and write them (or z alone on the last pass): 32n per pass
+    passes = (degree + 3) // 4
+    return float(48 * degree * n if model == "as_written" else 32 * passes * n)
 
 
-def proj_alg_bytes(n: int, steps_js: list[int]) -> float:
-    """Algorithmic bytes of the launches of the dominant kernel (fused
-    projection): per step j, 2j launches; 2j-1 carry AXPY (24n) + dot (16n),
-    the last AXPY (24n) + norm (8n)."""
-    return float(sum((2 * j - 1) * 40 * n + 32 * n for j in steps_js))
+def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str) -> float:
+    """One full restart cycle of m Arnoldi steps."""
+    if model == "as_written":  # SURVEY 8(d): per step (40 + 80 j) n, cycle start 64n, update 8(m+2)n
+        if method == "hh":
+            b = sum((64 + 80 * j) * n for j in range(1, m + 1)) + 64 * n + 8 * (m + 2) * n + 40 * m * n
+        else:
+            b = sum((40 + 80 * j) * n for j in range(1, m + 1)) + 64 * n + 8 * (m + 2) * n
+        return float(b + (m + 1) * prec_bytes(n, prec, degree, model))
+    st = 24 * n  # stencil fused with the first dot: read V_j and V_1, write w
+    if method == "hh":
+        b = sum(hh_chain_bytes(n, j, model) * 2 + st + 40 * n for j in range(1, m + 1))
+        b += hh_chain_bytes(n, m, model) + 24 * n + 40 * n
+    else:
+        b = sum(mgs_step_bytes(n, j, model) + st for j in range(1, m + 1))
+        b += 40 * n + 8 * (m + 2) * n  # cycle start (b - A x, norm, V_1) + x update
+    return float(b + (m + 1) * prec_bytes(n, prec, degree, model))
 
 
-def res_alg_bytes(n: int, j: int) -> float:
-    """Algorithmic bytes of one resident-step launch (step j): the reference's
-    MGS-R cascade as written, 2j x (dot 16n + AXPY 24n), + norm 8n + scale 16n
-    (SURVEY 8(d) per-step model without the 16n stencil, which is its own launch)."""
-    return float((80 * j + 24) * n)
+# ------------------------------------------------------------- CPU baseline ---
+def cpu_info() -> dict:
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    share = min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff
+    return {"nproc": os.cpu_count(), "affinity": aff, "OMP_NUM_THREADS": omp or None, "cpu_model": model,
+            "all_cores": share}
 
 
-def cpu_baseline(N: int, m: int, prec: str, degree: int, sample_steps: int, threads: int) -> dict:
-    """Reference CPU path (the oracle, a loop-for-loop restatement of
-    gmres_mgsr_omp) on this host: the first `sample_steps` Arnoldi steps of
-    cycle 1 of the same workload; converted to full-cycle it/s through the
-    same byte model (its per-step cost grows with j like the GPU's)."""
-    from oracle import oracle as orc
-
-    orc.build()
-    b = orc.rhs_ones(N)
-    kind = {"identity": orc.PREC_IDENTITY, "cbpr2": orc.PREC_CBPR2, "cheb": orc.PREC_CHEB}[prec]
-    t0 = time.perf_counter()
-    r = orc.gmres_mgsr(b, N, m, prec=kind, degree=degree, variant=orc.MGSR_OMP, max_cycles=1,
-                       step_limit=sample_steps, threads=threads)
-    t1 = time.perf_counter()
-    st = r.step_times
-    # per-step times from the oracle's own omp_get_wtime stamps
-    dt = np.diff(st)
-    steps_timed = list(range(2, sample_steps + 1))
-    n = N * N
-    bytes_timed = sum((40 + 80 * j) * n for j in steps_timed)
-    if prec == "cbpr2":
-        bytes_timed += 64 * n * len(steps_timed)
-    elif prec == "cheb":
-        bytes_timed += (16 + 48 * degree) * n * len(steps_timed)
-    gbps = bytes_timed / dt.sum() / 1e9
-    it_s = gbps * 1e9 / (alg_bytes_cycle(n, m, prec, degree) / m)
-    return {"value": round(it_s, 4), "unit": "Arnoldi it/s", "cores": threads, "kind": "port",
-            "gbps_alg": round(gbps, 2),
-            "sample": f"oracle/gmres_oracle.c (gmres_mgsr_omp restatement, OpenMP {threads} threads) on "
-                      f"{N}^2 m={m} prec={prec}: Arnoldi steps 2..{sample_steps} of cycle 1 "
-                      f"({t1 - t0:.1f} s wall incl. setup), {gbps:.1f} GB/s algorithmic, scaled to a full "
-                      f"cycle by the SURVEY 8(d) byte model"}
+def _extrapolate(step_t: dict, c0: float, m: int) -> tuple[float, str]:
+    """Cycle time from step stamps of a cut run: step durations d_j = t_{j+1}
+    - t_j are linear in j (2j dot+AXPY pairs); least-squares a + b j over the
+    sampled steps, summed over j = 1..m, plus the cycle start as measured and
+    the x update priced at (m+2)/10 of one (dot+AXPY pair) increment b."""
+    js = sorted(step_t)
+    d = {j: step_t[j + 1] - step_t[j] for j in js if j + 1 in step_t}
+    xs = np.array(sorted(d), dtype=float)
+    ys = np.array([d[int(j)] for j in xs])
+    if len(xs) >= 3:
+        b, a = np.polyfit(xs[1:], ys[1:], 1)  # step 1 pays first touches
+    else:
+        b, a = 0.0, float(ys.mean())
+    start = step_t[js[0]] - c0
+    t = start + sum(a + b * j for j in range(1, m + 1)) + max(b, 0.0) * (m + 2) / 10.0
+    return float(t), f"steps 1..{int(xs[-1]) + 1} timed, step cost fitted a + b j (a={a:.4g} s, b={b:.4g} s)"
 
 
+def cpu_baseline(N: int, m: int, prec: str, degree: int, method: str, cap_all: float, cap_one: float) -> dict:
+    """The reference CPU path timed on this host (rank 0, N = 1 only):
+    oracle/_ref/ref_driver = the reference's own gmres_mgsr_omp / gmres_hh_omp
+    (kind "reference"); Chebyshev(k) does not exist in the reference, so that
+    config times the restatement (kind "port").  All cores of this process's
+    CPU share (OMP_PROC_BIND=close, OMP_PLACES=cores) for one full cycle when
+    it finishes within cap_all seconds (else a fitted sample), plus 1 core on a
+    bounded sample."""
+    from oracle import refrun
+
+    info = cpu_info()
+    env = {"OMP_PROC_BIND": "close", "OMP_PLACES": "cores"}
+    legs = {}
+    use_ref = refrun.available() and prec in ("identity", "cbpr2")
+    solver = ("hh_omp" if prec == "identity" else "hh_prec_omp") if method == "hh" else "mgsr_omp"
+    for name, thr, cap in (("all_cores", info["all_cores"], cap_all), ("one_core", 1, cap_one)):
+        t0 = time.perf_counter()
+        if use_ref:
+            e = dict(env, REF_TIME_CAP=str(cap))
+            r = refrun.run(solver, N, m, prec, threads=thr, max_cycles=1, env=e, timeout=cap + 600)
+            c0 = r.cycle_t[0]
+            if len(r.cycle_t) >= 2:  # full cycle: stamps at the starts of cycles 1 and 2
+                t_cyc, how = r.cycle_t[1] - c0, "one full cycle timed (omp_get_wtime stamps of cycles 1 and 2)"
+            else:
+                t_cyc, how = _extrapolate(r.step_t, c0, m)
+            thr_used = r.threads
+        else:
+            from oracle import oracle as orc
+
+            kind = {"identity": orc.PREC_IDENTITY, "cbpr2": orc.PREC_CBPR2, "cheb": orc.PREC_CHEB}[prec]
+            steps = m if name == "all_cores" else 12
+            rr = orc.gmres_mgsr(orc.rhs_ones(N), N, m, prec=kind, degree=degree, variant=orc.MGSR_OMP,
+                                max_cycles=1, step_limit=steps, threads=thr)
+            st = {j + 1: float(t) for j, t in enumerate(rr.step_times) if t > 0}
+            t_cyc, how = _extrapolate(st, 0.0, m)
+            thr_used = thr
+        legs[name] = {"threads": thr_used, "cycle_s": round(t_cyc, 3), "it_s": round(m / t_cyc, 4),
+                      "how": how, "wall_s": round(time.perf_counter() - t0, 1)}
+    a = legs["all_cores"]
+    return {"value": a["it_s"], "unit": "Arnoldi it/s", "cores": a["threads"],
+            "kind": "reference" if use_ref else "port",
+            "sample": (f"{'oracle/_ref/ref_driver (the reference src/*.f90 built by oracle/Makefile.ref)' if use_ref else 'oracle/gmres_oracle.c (restatement; Chebyshev(k) is not in the reference)'} "
+                       f"{solver} on {N}^2 m={m} prec={prec}, b = A*1, x0 = 0; all cores: {a['how']}; "
+                       f"1 core: {legs['one_core']['how']}"),
+            "one_core": legs["one_core"], "all_cores": a,
+            "hbm_gbps_alg_as_written": round(cycle_bytes(N * N, m, prec, degree, method, "as_written")
+                                             / a["cycle_s"] / 1e9, 1),
+            "host": info, "calibration": "profiles/r02/cpu_calibration.json"}
+
+
+# ------------------------------------------------------------- launcher -----
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus: int, argv: list[str]) -> dict:
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)]
+    cmd += [a for a in argv if a != "--plan-only"]
+    return {"launcher": "torch.distributed.run", "ranks": gpus, "cmd": cmd,
+            "env": {"HSA_ENABLE_IPC_MODE_LEGACY": "0"}}
+
+
+def maybe_self_launch(args, argv: list[str]) -> None:
+    """N > 1 without a launcher: start one rank per GPU as child processes
+    (never exec from a process that may have touched the GPU) and exit with
+    their status."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        if args.plan_only:
+            print(json.dumps({"launcher": None, "ranks": int(os.environ.get("WORLD_SIZE", "1"))}))
+            sys.exit(0)
+        return
+    plan = launch_plan(args.gpus, argv)
+    if args.plan_only:
+        print(json.dumps(plan))
+        sys.exit(0)
+    import torch
+
+    vis = torch.cuda.device_count()  # counting devices does not initialise them on this image
+    if vis < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but only {vis} GPU(s) visible", file=sys.stderr)
+        sys.exit(2)
+    env = dict(os.environ, **plan["env"])
+    p = subprocess.run(plan["cmd"], env=env)
+    sys.exit(p.returncode)
+
+
+# ------------------------------------------------------------- device exchange
 def setup_xgmi(ctx, dist, world: int, rank: int, required: bool):
     """Map every rank's exchange region (IPC handles over the gloo control
     plane) and run the collective self-test; every rank must pass, else all
@@ -131,6 +253,70 @@ def setup_xgmi(ctx, dist, world: int, rank: int, required: bool):
     return None
 
 
+def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int) -> dict | None:
+    """Dominant kernel: its algorithmic bytes per launch (fused-minimum model)
+    over its average launch time from HIP events on the context stream."""
+    m = args.m
+    if not prof or prof.get("res", (0.0, 0))[1] == 0:
+        if not prof or prof["proj"][1] == 0:
+            return None
+        # launch-per-projection path (RCCL multi-rank, or after a fallback)
+        ms, launches = prof["proj"]
+        S = 1 if args.method == "hh" else max(1, args.prof_every)
+        steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
+        nproj = sum(2 * j for j in steps_js)
+        fused, written = 32.0 * nloc * nproj, 40.0 * nloc * nproj
+        kname = "gk::k_proj (AXPY_i fused with dot_{i+1}, one launch per projection)"
+        timing = f"HIP events around every projection launch of steps j % {S} == 0 of the timed cycles"
+        per_proj = ms * 1e3 / launches
+    else:
+        ms, launches = prof["res"]
+        if args.method == "hh":
+            steps_js = list(range(1, m + 1)) * cycles
+            chains = [j for j in steps_js for _ in (0, 1)] + [m] * cycles
+            fused = sum(hh_chain_bytes(nloc, L, "fused") for L in chains)
+            written = sum(hh_chain_bytes(nloc, L, "as_written") for L in chains)
+            nproj = sum(chains)
+            kname = ("gk::k_mgs_wres / k_mgs_res in reflection mode (RES_HH_DOWN / RES_HH_UP: a chain of j "
+                     "Householder reflections per persistent launch)")
+            timing = "HIP events on the context stream around every resident launch of the timed cycles"
+        else:
+            S = max(1, args.prof_every)
+            steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
+            fused = sum(mgs_step_bytes(nloc, j, "fused") for j in steps_js)
+            written = sum(mgs_step_bytes(nloc, j, "as_written") for j in steps_js)
+            nproj = sum(2 * j for j in steps_js)
+            kname = ("gk::k_mgs_wres / k_mgs_res (resident MGS-R step: 2j fused projections + norm + scale, one "
+                     "persistent launch per Arnoldi step)")
+            timing = f"HIP events on the context stream around the step launch of steps j % {S} == 0 of the timed cycles"
+        per_proj = ms * 1e3 / nproj
+    secs = ms / 1e3
+    ach = fused / secs / 1e9
+    roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None, "model": "fused minimum (DESIGN.md §3)",
+            "kernel": kname, "launches": launches, "avg_launch_us": round(ms * 1e3 / launches, 2),
+            "alg_bytes_per_launch": round(fused / launches), "per_projection_us": round(per_proj, 2),
+            "alg_as_written_bytes_per_launch": round(written / launches),
+            "alg_as_written_frac": round(written / secs / 1e9 / HBM_PEAK_GBPS, 4),
+            "timing": timing, "per_kernel_ms_sampled": {k: round(v[0], 3) for k, v in prof.items()}}
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    key = f"{args.grid}_{m}_{args.prec}_{args.method}_{world}_res"
+    if os.path.exists(tf) and prof.get("res", (0, 0))[1] > 0 and args.method == "mgsr":
+        pm = json.load(open(tf)).get(key)
+        if pm and "per_step" in pm:
+            per_step = {int(k): v for k, v in pm["per_step"].items()}
+            if all(j in per_step for j in set(steps_js)):
+                tb = sum(per_step[j] for j in steps_js) / len(steps_js)
+                roof["traffic"] = round(tb)
+                roof["traffic_source"] = pm["source"]
+                roof["physical"] = {"fabric_GBps": round(tb * launches / secs / 1e9, 1),
+                                    "traffic_over_alg": round(tb * launches / fused, 3),
+                                    "note": "FETCH_SIZE (x2, gfx950) + WRITE_SIZE at the same steps j: L2<->fabric "
+                                            "bytes, Infinity-Cache hits included"}
+    return roof
+
+
+# ------------------------------------------------------------------- main ---
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -142,23 +328,27 @@ def main() -> None:
     ap.add_argument("--degree", type=int, default=8)
     ap.add_argument("--method", default="mgsr", choices=["mgsr", "hh"])
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=90)
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-cap", type=float, default=45.0,
+                    help="seconds: all-core reference leg runs a full cycle if it finishes within this, else a sample")
+    ap.add_argument("--cpu-cap-one", type=float, default=15.0, help="seconds of the 1-core sample")
     ap.add_argument("--no-prof", action="store_true", help="no HIP-event kernel timing in the timed region")
     ap.add_argument("--collective", default="auto", choices=["auto", "rccl", "xgmi"],
                     help="N>1: RCCL calls, or the device exchange over xGMI (auto: device exchange if its "
                          "self-test passes on every rank, else RCCL)")
     ap.add_argument("--prof-every", type=int, default=16,
                     help="HIP events around the launches of every S-th Arnoldi step (1 = all)")
+    ap.add_argument("--plan-only", action="store_true", help="print the multi-GPU launch plan and exit")
     args = ap.parse_args()
+    maybe_self_launch(args, sys.argv[1:])
 
     import torch  # device plumbing + gloo control plane only
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -198,29 +388,35 @@ def main() -> None:
         if dist is not None:
             dist.barrier()
 
-    def guarded_warmup() -> bool:
-        ok = 1
+    def guarded_warmup() -> tuple[bool, str]:
+        ok, why = 1, ""
         try:
             if args.warmup > 0:
                 run(args.warmup)
         except Exception as e:  # noqa: BLE001 - every rank reports, then all agree below
+            why = str(e)
             print(f"rank {rank}: warmup failed: {e}", file=sys.stderr)
             ok = 0
         if dist is not None:
             t = torch.tensor([ok], dtype=torch.int32)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             ok = int(t.item())
-        return ok == 1
+        return ok == 1, why
 
-    if not guarded_warmup():
-        # Fallback, decided by all ranks together: the launch-per-projection path
-        # (and RCCL instead of the device exchange when that was in use).
+    fallback = None
+    ok, why = guarded_warmup()
+    if not ok:
+        # Fallback, decided by all ranks together and REPORTED in the JSON line:
+        # the launch-per-projection path (and RCCL instead of the device exchange).
+        fallback = {"reason": why[:300] or "a peer rank failed its warmup", "to": "launch-per-projection path"}
         if collective == "xgmi-device-exchange" and args.collective == "auto":
             ctx.xchg_enable(False)
-            collective = "rccl (device exchange failed in warmup)"
+            collective = "rccl"
+            fallback["to"] += " + RCCL (device exchange failed in warmup)"
         ctx.tune(8, 0)  # GK_TUNE_RES off
-        if not guarded_warmup():
-            raise RuntimeError("warmup failed on the fallback path too")
+        ok, why = guarded_warmup()
+        if not ok:
+            raise RuntimeError(f"warmup failed on the fallback path too: {why}")
     if not args.no_prof:
         ctx.profile(1 if args.method == "hh" else max(1, args.prof_every))
         ctx.profile_reset()
@@ -231,6 +427,7 @@ def main() -> None:
     t1 = time.perf_counter()
     prof = ctx.profile_read() if not args.no_prof else {}
     resid = ctx.true_residual()  # outside the timed region; same value at any N
+    comm = ctx.comm_info()
     elapsed = t1 - t0
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -241,94 +438,14 @@ def main() -> None:
 
     if rank == 0:
         n = N * N
-        nloc = ctx.nloc
         it_s = iters / elapsed
-        bytes_cycle = alg_bytes_cycle(n, m, args.prec, args.degree)
-        gbps_alg = bytes_cycle * cycles / elapsed / 1e9 if cycles == args.steps else None
-        roof = None
-        if prof and prof.get("res", (0.0, 0))[1] > 0:
-            # resident MGS-R step: one launch = the 2j projections + norm + scale of step j
-            ms, launches = prof["res"]
-            if args.method == "hh":
-                # every launch sampled (profile(1)): per step j a RES_HH_DOWN chain (v_j = P_1..P_j e_j)
-                # and a RES_HH_UP chain (w = P_j..P_1 A v_j), j reflections of 40n each
-                # (gmres_hh.f90:269-304); per cycle one more chain of n_out = m (x update, :361-373)
-                steps_js = list(range(1, m + 1)) * cycles
-                palg = float(sum(2 * j * 40 * nloc for j in steps_js) + cycles * m * 40 * nloc)
-                nproj = sum(2 * j for j in steps_js) + cycles * m
-                kname = ("gk::k_mgs_res / k_mgs_wres in reflection mode (RES_HH_DOWN / RES_HH_UP: a chain of j "
-                         "Householder reflections, one persistent launch per chain)")
-                timing = "HIP events on the context stream around every resident launch of the timed cycles"
-            else:
-                S = max(1, args.prof_every)
-                steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
-                palg = float(sum(res_alg_bytes(nloc, j) for j in steps_js))
-                nproj = sum(2 * j + 1 for j in steps_js)
-                kname = ("gk::k_mgs_res (resident MGS-R step: 2j fused projections + norm + scale, one "
-                         "persistent launch per Arnoldi step)")
-                timing = (f"HIP events on the context stream around the step launch of steps j % {S} == 0 "
-                          f"of the timed cycles")
-            achieved = palg / (ms / 1e3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "kernel": kname,
-                    "launches": launches, "avg_launch_us": round(ms * 1e3 / launches, 2),
-                    "alg_bytes_per_launch": round(palg / launches),
-                    "per_projection_us": round(ms * 1e3 / nproj, 2),
-                    "timing": timing,
-                    "per_kernel_ms_sampled": {k: round(v[0], 3) for k, v in prof.items()}}
-            tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            key = f"{N}_{m}_{args.prec}_{args.method}_{world}_res"
-            if os.path.exists(tf):
-                pm = json.load(open(tf))
-                if key in pm:
-                    # PMC bytes per launch are linear in the projection count: a + b 2j
-                    a0, b0 = pm[key]["bytes_fixed"], pm[key]["bytes_per_projection"]
-                    tb = sum(a0 + b0 * 2 * j for j in steps_js) / len(steps_js)
-                    roof["traffic"] = round(tb)
-                    roof["traffic_source"] = pm[key]["source"]
-                    roof["physical"] = {"fabric_GBps": round(tb * launches / (ms / 1e3) / 1e9, 1),
-                                        "bytes_per_projection": round(b0)}
-        elif prof and prof["proj"][1] > 0:
-            ms, launches = prof["proj"]
-            S = 1 if args.method == "hh" else max(1, args.prof_every)
-            steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
-            if args.method == "hh":
-                # HH: 2j reflections/step (j on v_j incl. a leading dot, j on w), 40n each
-                palg = float(sum(2 * j * 40 * nloc for j in steps_js))
-            else:
-                palg = proj_alg_bytes(nloc, steps_js)
-            achieved = palg / (ms / 1e3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "kernel": "gk::k_proj (fused MGS-R AXPY_i + dot_{i+1})", "launches": launches,
-                    "avg_launch_us": round(ms * 1e3 / launches, 2),
-                    "alg_bytes_per_launch": round(palg / launches),
-                    "timing": f"HIP events on the context stream around every launch of steps j % {S} == 0 "
-                              f"of the timed cycles (launch cost is independent of j)",
-                    "per_kernel_ms_sampled": {k: round(v[0], 3) for k, v in prof.items()}}
-            tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(tf):
-                try:
-                    pm = json.load(open(tf))
-                    key = f"{N}_{m}_{args.prec}_{args.method}_{world}"
-                    if key in pm:
-                        tb = pm[key]["hbm_bytes_per_launch"]
-                        roof["traffic"] = round(tb)
-                        roof["traffic_source"] = pm[key]["source"]
-                        avg_s = ms / 1e3 / launches
-                        roof["physical"] = {
-                            "fabric_GBps": round(tb / avg_s / 1e9, 1),
-                            "fabric_frac_of_hbm_peak": round(tb / avg_s / 1e9 / HBM_PEAK_GBPS, 4),
-                            "note": "frac > 1 is algorithmic: the reference's op sequence moves 40 B/unknown per "
-                                    "dot+AXPY pair, the fused kernel moves 32 B/unknown (traffic), and w "
-                                    "(128 MiB at 4096^2) is re-read from the 256 MiB Infinity Cache"}
-                except Exception:
-                    pass
+        full = cycles == args.steps and res.n_out == m
+        b_fused = cycle_bytes(n, m, args.prec, args.degree, args.method, "fused") * cycles
+        b_written = cycle_bytes(n, m, args.prec, args.degree, args.method, "as_written") * cycles
+        roof = roofline_entry(prof, args, ctx.nloc, cycles, world)
         cpu = None
         if not args.no_cpu and world == 1:
-            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(N, m, args.prec, args.degree, args.cpu_steps, thr)
+            cpu = cpu_baseline(N, m, args.prec, args.degree, args.method, args.cpu_cap, args.cpu_cap_one)
         prec_name = {"identity": "no precond", "cbpr2": "cbpr2", "cheb": f"Chebyshev({args.degree})"}[args.prec]
         out = {
             "metric": METRIC,
@@ -346,10 +463,14 @@ def main() -> None:
             "config": {"workload": f"{N}x{N} Poisson-2D fp64, GMRES-{args.method.upper()} m={m}, {prec_name}",
                        "grid": N, "m": m, "precond": args.prec, "method": args.method,
                        "step": "one GMRES(m) restart cycle", "parallelism": f"row-block slabs x{world}",
-                       "collective": collective, "arnoldi_iters": iters},
+                       "collective": collective, "comm_ranks_seen": comm["nranks"], "comm_kind": comm["kind"],
+                       "arnoldi_iters": iters},
+            "fallback": fallback,
             "check": {"true_rel_residual_after_timed_cycles": resid},
-            "hbm_gbps_alg": round(gbps_alg, 1) if gbps_alg else None,
-            "cycle_roofline_frac": round(gbps_alg / HBM_PEAK_GBPS, 4) if gbps_alg else None,
+            "hbm_gbps_fused": round(b_fused / elapsed / 1e9, 1) if full else None,
+            "cycle_roofline_frac": round(b_fused / elapsed / 1e9 / HBM_PEAK_GBPS, 4) if full else None,
+            "hbm_gbps_alg_as_written": round(b_written / elapsed / 1e9, 1) if full else None,
+            "alg_as_written_frac": round(b_written / elapsed / 1e9 / HBM_PEAK_GBPS, 4) if full else None,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -25,6 +25,7 @@ GK_TUNE_RES, GK_TUNE_RES_R2, GK_TUNE_RES_SHARE, GK_TUNE_RES_TIMEOUT_MS = 8, 9, 1
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES = range(7)
 KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res"]
+COMM_KINDS = {0: None, 1: "rccl", 2: "local-group", 3: "xgmi-device-exchange"}
 
 c_int, c_double, c_ll, c_vp = ctypes.c_int, ctypes.c_double, ctypes.c_longlong, ctypes.c_void_p
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -52,6 +53,7 @@ _SIGS = {
     "gk_comm_unique_id": (c_int, [ctypes.c_char_p]),
     "gk_comm_init": (c_int, [c_vp, c_int, c_int, c_int, ctypes.c_char_p]),
     "gk_local_size": (c_int, [c_vp, ctypes.POINTER(c_ll)]),
+    "gk_comm_info": (c_int, [c_vp, _ip, _ip]),
     "gk_group_create": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "gk_group_destroy": (c_int, [c_vp]),
     "gk_comm_init_local": (c_int, [c_vp, c_vp, c_int, c_int]),

@@ -1340,6 +1340,25 @@ int gk_xchg_selftest(gk_ctx *c, int timeout_ms) {
     return GK_OK;
 }
 
+int gk_comm_info(gk_ctx *c, int *kind, int *nranks_seen) {
+    if (c == nullptr || kind == nullptr || nranks_seen == nullptr) return set_err(GK_ERR_ARG, "null argument");
+    *kind = GK_COMM_NONE;
+    *nranks_seen = 1;
+    if (c->xs_on) {
+        *kind = GK_COMM_XGMI;
+        int k = 0;
+        for (int r = 0; r < c->nranks; ++r) k += c->xs_peers.p[r] != nullptr;
+        *nranks_seen = k;
+    } else if (c->lg != nullptr) {
+        *kind = GK_COMM_LOCAL;
+        *nranks_seen = c->lg->n;
+    } else if (c->comm != nullptr) {
+        *kind = GK_COMM_RCCL;
+        NCCLCHK(ncclCommCount(c->comm, nranks_seen));
+    }
+    return GK_OK;
+}
+
 int gk_local_size(gk_ctx *c, long long *nloc) {
     CHK(check_ctx(c));
     *nloc = c->nloc;

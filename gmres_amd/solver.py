@@ -158,6 +158,13 @@ class Context:
     def xchg_enable(self, on: bool) -> None:
         nat.check(nat.hip().gk_xchg_enable(self._h, int(bool(on))), "gk_xchg_enable")
 
+    def comm_info(self) -> dict:
+        """The collective back-end actually in use and the rank count its
+        communicator reports (gk_comm_info)."""
+        k, nr = ctypes.c_int(), ctypes.c_int()
+        nat.check(nat.hip().gk_comm_info(self._h, ctypes.byref(k), ctypes.byref(nr)), "gk_comm_info")
+        return {"kind": nat.COMM_KINDS.get(k.value, k.value), "nranks": nr.value}
+
     def xchg_selftest(self, timeout_ms: int = 5000) -> bool:
         """Collective self-test of the device exchange; False (and the
         exchange disabled on this rank) when it fails."""

@@ -104,6 +104,15 @@ int gk_xchg_local(gk_ctx *ctx);
 int gk_xchg_enable(gk_ctx *ctx, int on);
 int gk_xchg_selftest(gk_ctx *ctx, int timeout_ms);
 int gk_local_size(gk_ctx *ctx, long long *nloc);
+/* What this context's collectives actually run on: kind = GK_COMM_NONE (single
+ * rank), GK_COMM_RCCL, GK_COMM_LOCAL (gk_group) or GK_COMM_XGMI (device
+ * exchange on); nranks_seen = the communicator's own rank count (ncclCommCount
+ * for RCCL, the mapped exchange regions for the device exchange). */
+#define GK_COMM_NONE 0
+#define GK_COMM_RCCL 1
+#define GK_COMM_LOCAL 2
+#define GK_COMM_XGMI 3
+int gk_comm_info(gk_ctx *ctx, int *kind, int *nranks_seen);
 
 /* Preconditioner: kind GK_PREC_*, params (cbpr2: params[0..1] as
  * chebyshev.f90:19-25; CHEB: interval ends params[0..1]), degree (CHEB only). */

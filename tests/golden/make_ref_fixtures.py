@@ -1,0 +1,108 @@
+"""Generate tests/golden/reference_runs.json + reference_x.npz by running the
+REFERENCE itself (oracle/_ref/ref_driver: the reference's own Fortran solver
+modules compiled from /root/reference/src, see oracle/Makefile.ref).
+
+Build container only (needs the compiled reference).  The fixtures are data:
+per-cycle true residuals, final_err(1:n_out), v_err, iteration counts, x (full
+at N <= 64).  Run:  python tests/golden/make_ref_fixtures.py [--quick]
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import refrun  # noqa: E402
+
+# (key, solver, N, m, prec, threads, max_cycles)
+SMALL = [
+    ("mgsr_mf_identity_32_m10", "mgsr_mf", 32, 10, "identity", 1, 0),
+    ("mgsr_mf_identity_32_m30", "mgsr_mf", 32, 30, "identity", 1, 0),
+    ("mgsr_mf_identity_64_m20", "mgsr_mf", 64, 20, "identity", 1, 0),
+    ("mgsr_mf_identity_128_m30", "mgsr_mf", 128, 30, "identity", 1, 0),
+    ("mgsr_omp_identity_128_m30", "mgsr_omp", 128, 30, "identity", 1, 0),
+    ("mgsr_mf_cbpr2_64_m20", "mgsr_mf", 64, 20, "cbpr2", 1, 0),
+    ("mgsr_omp_cbpr2_32_m10", "mgsr_omp", 32, 10, "cbpr2", 1, 0),
+    ("mgsr_omp_cbpr2_64_m20", "mgsr_omp", 64, 20, "cbpr2", 1, 0),
+    ("mgsr_omp_cbpr2_128_m30", "mgsr_omp", 128, 30, "cbpr2", 1, 0),
+    ("hh_omp_identity_32_m10", "hh_omp", 32, 10, "identity", 1, 0),
+    ("hh_omp_identity_64_m20", "hh_omp", 64, 20, "identity", 1, 0),
+    ("hh_omp_identity_128_m30", "hh_omp", 128, 30, "identity", 1, 0),
+    ("hh_prec_omp_cbpr2_32_m10", "hh_prec_omp", 32, 10, "cbpr2", 1, 0),
+    ("hh_prec_omp_cbpr2_64_m20", "hh_prec_omp", 64, 20, "cbpr2", 1, 0),
+    ("hh_prec_omp_cbpr2_128_m30", "hh_prec_omp", 128, 30, "cbpr2", 1, 0),
+    ("pcg_omp_identity_48", "pcg_omp", 48, 5000, "identity", 1, 0),
+    ("pcg_omp_cbpr2_48", "pcg_omp", 48, 5000, "cbpr2", 1, 0),
+    ("pbicgstab_omp_identity_48", "pbicgstab_omp", 48, 5000, "identity", 1, 0),
+    ("pbicgstab_omp_cbpr2_48", "pbicgstab_omp", 48, 5000, "cbpr2", 1, 0),
+    # capped serial histories at config-2 size (SURVEY 8c known answers)
+    ("mgsr_mf_identity_1024_m95_3cyc", "mgsr_mf", 1024, 95, "identity", 1, 3),
+    ("mgsr_mf_cbpr2_1024_m95_3cyc", "mgsr_mf", 1024, 95, "cbpr2", 1, 3),
+]
+THREADED = [
+    ("mgsr_omp_identity_128_m30_t8", "mgsr_omp", 128, 30, "identity", 8, 0),
+    ("hh_omp_identity_128_m30_t8", "hh_omp", 128, 30, "identity", 8, 0),
+    ("hh_omp_identity_1024_m95_3cyc_t8", "hh_omp", 1024, 95, "identity", 8, 3),
+    ("mgsr_omp_identity_1024_m95_3cyc_t8", "mgsr_omp", 1024, 95, "identity", 8, 3),
+    # full-size configs (1 cycle each): 1, 3 (cbpr2 reference leg), 5
+    ("mgsr_omp_identity_4096_m95_1cyc_t8", "mgsr_omp", 4096, 95, "identity", 8, 1),
+    ("mgsr_omp_cbpr2_4096_m95_1cyc_t8", "mgsr_omp", 4096, 95, "cbpr2", 8, 1),
+    ("hh_omp_identity_4096_m95_1cyc_t8", "hh_omp", 4096, 95, "identity", 8, 1),
+]
+
+
+def record(key, solver, N, m, prec, threads, max_cycles):
+    t0 = time.time()
+    r = refrun.run(solver, N, m, prec, threads=threads, max_cycles=max_cycles, want_x=N <= 64)
+    d = {"solver": solver, "N": N, "m": m, "prec": prec, "threads": r.threads, "max_cycles": max_cycles,
+         "cut": r.cut, "hist_res": r.hist_res.tolist(), "wall_s": round(time.time() - t0, 2)}
+    if r.krylov is not None:
+        d["iterations"], d["res"] = r.krylov
+        d["x_err"] = list(r.x_err)
+    elif not r.cut:
+        d.update(iterations=r.iterations, cycles=r.cycles_out, n_out=r.n_out, final_err=r.final_err.tolist(),
+                 v_err=r.v_err.tolist(), x_err=list(r.x_err), time_s=r.time)
+    print(f"{key}: {time.time() - t0:.1f} s", flush=True)
+    return key, d, r.x
+
+
+def main() -> None:
+    quick = "--quick" in sys.argv
+    refrun.build()
+    small = [c for c in SMALL if not quick or c[2] <= 128]
+    out, xs = {}, {}
+    with ThreadPoolExecutor(6) as ex:
+        for key, d, x in ex.map(lambda c: record(*c), small):
+            out[key] = d
+            if x is not None:
+                xs[key] = x
+    for c in THREADED:
+        if quick and c[2] > 128:
+            continue
+        key, d, x = record(*c)
+        out[key] = d
+        if x is not None:
+            xs[key] = x
+    meta = {"_source": "oracle/_ref/ref_driver: the reference's own src/*.f90 (AlexanderGSC/gmres) compiled "
+                       "by oracle/Makefile.ref (amdflang 22, -O3 -fopenmp -funroll-loops; interfaces.f90 "
+                       "with the one-line import fix), driven through the stencil_vector/precond seam by "
+                       "oracle/ref_driver.f90; b = A*1, x0 = 0, tol 1e-15 (CG/BiCGSTAB 1e-9), params (8.2, 0.2)",
+            "_generator": "tests/golden/make_ref_fixtures.py"}
+    path = os.path.join(HERE, "reference_runs.json")
+    old = json.load(open(path)) if os.path.exists(path) and quick else {}
+    old.update(out)
+    old.update(meta)
+    json.dump(dict(sorted(old.items())), open(path, "w"), indent=1)
+    np.savez_compressed(os.path.join(HERE, "reference_x.npz"), **xs)
+
+
+if __name__ == "__main__":
+    main()

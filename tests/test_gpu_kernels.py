@@ -51,9 +51,16 @@ def test_poisson5_slabs_with_halos(oracle, N, nranks):
         assert np.array_equal(ys.cpu().numpy(), ref[line0 * N:(line0 + nl) * N])
 
 
-@pytest.mark.parametrize("N", [16, 64, 129, 256])
-@pytest.mark.parametrize("kind,degree", [("cbpr2", 1), ("cheb", 1), ("cheb", 8), ("identity", 1)])
+PREC_CASES = [("cbpr2", 1), ("identity", 1)] + [("cheb", k) for k in range(1, 9)]
+
+
+@pytest.mark.parametrize("N", [16, 64, 129, 130, 256])
+@pytest.mark.parametrize("kind,degree", PREC_CASES)
 def test_precond_bitexact(oracle, N, kind, degree):
+    """Every Chebyshev degree 1..8: one temporal-blocked pass of L = k levels
+    (k <= 4) or two passes (4 + k-4) when N is even; 130 and 256 have more
+    than one 64-line tile (ragged last tile at 130); odd N takes the per-sweep
+    kernels."""
     import gmres_amd.solver as S
 
     rng = np.random.default_rng(N + degree)
@@ -98,3 +105,56 @@ def test_unaligned_pointer_rejected():
     x = torch.zeros(65, dtype=torch.float64, device="cuda")
     with pytest.raises(GkError):
         S.dot(x[1:], x[1:], x[:1])
+
+
+def _ctx_col(c, k):
+    """V(:,k+1) of a context, through the device vector API (copy to x)."""
+    from gmres_amd import _native as nat
+
+    nat.check(nat.hip().gk_vec_lincomb(c.handle, 0, 0, 2 + k, 0, 0, 0.0, 0.0), "gk_vec_lincomb")
+    return c.get_x()
+
+
+@pytest.mark.parametrize("N,degree", [(130, 3), (256, 6), (256, 8)])
+def test_fused_chebyshev_norm_epilogue(oracle, N, degree):
+    """The ACC_NORM last pass (cycle start: w = M^-1 b, beta = ||w||, V(:,1) = w/beta):
+    w is bit-exact, so V(:,1) equals oracle_w / beta_gpu bit for bit, and beta is
+    the oracle's norm to summation-order noise -- with the fused passes and the
+    per-sweep kernels alike (GK_TUNE_CHEB_FUSED = 6)."""
+    import gmres_amd as ga
+
+    w = oracle.precond(oracle.PREC_CHEB, oracle.rhs_ones(N), N, params=(8.2, 0.2), degree=degree)
+    bref = float(np.sqrt(np.sum(w * w)))
+    for fused in (1, 0):
+        with ga.Context(N, 10) as c:
+            c.tune(6, fused)
+            c.tune(8, 0)  # launch path: the cycle start is the same either way
+            c.set_precond("cheb", (8.2, 0.2), degree)
+            c.set_rhs_ones()
+            beta = c.mgs_cycle_start()
+            v1 = _ctx_col(c, 0)
+        assert beta == pytest.approx(bref, rel=1e-14)
+        assert np.array_equal(v1, w / beta)
+
+
+@pytest.mark.parametrize("N,degree", [(130, 5), (256, 8)])
+def test_fused_chebyshev_dot_epilogue_step(N, degree):
+    """The ACC_DOT last pass inside an Arnoldi step (w = M^-1 A V(:,j) fused with
+    <w, V(:,1)>): fused passes vs per-sweep kernels give the same Hessenberg
+    columns and Krylov vectors for steps 1..4 up to the dot's summation order
+    (the two paths reduce over different workgroup grids, so the last bit of a
+    dot may differ; the element-wise w is bit-identical, test above)."""
+    import gmres_amd as ga
+
+    res = {}
+    for fused in (1, 0):
+        with ga.Context(N, 10) as c:
+            c.tune(6, fused)
+            c.set_precond("cheb", (8.2, 0.2), degree)
+            c.set_rhs_ones()
+            c.mgs_cycle_start()
+            cols = [c.mgs_step(j) for j in range(1, 5)]
+            res[fused] = (cols, _ctx_col(c, 4))
+    for a, b in zip(res[1][0], res[0][0]):
+        assert np.allclose(a, b, rtol=1e-12, atol=1e-15)
+    assert np.allclose(res[1][1], res[0][1], rtol=1e-10, atol=1e-14)

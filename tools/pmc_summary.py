@@ -31,27 +31,34 @@ def series(path, kernel):
 
 
 def res_fit(a):
-    """Least-squares fit of the per-launch bytes of the resident step kernel
-    against its projection count 2j (j = 1..probe_m, launch order)."""
+    """Per-launch bytes of the resident step kernel over ONE full cycle
+    (bench.py --steps 1 --warmup 0: launches j = 1..m in dispatch order):
+    recorded per step j (bench.py quotes the steps it samples, j % 16 == 0)
+    plus a least-squares line fixed + per_projection * 2j with its residual."""
     import numpy as np
 
     f = np.array(series(a.fetch, a.kernel)) * 2.0  # gfx950 FETCH_SIZE correction
     w = np.array(series(a.write, a.kernel))
     k = min(len(f), len(w))
-    x = np.array([2 * (i % a.probe_m + 1) for i in range(k)], dtype=float)
-    y = f[:k] + w[:k]
-    b, c = np.polyfit(x, y, 1)
+    if k < a.probe_m:
+        raise SystemExit(f"only {k} launches of {a.kernel!r} (expected {a.probe_m})")
+    y = f[: a.probe_m] + w[: a.probe_m]
+    js = np.arange(1, a.probe_m + 1)
+    b, c = np.polyfit(2 * js, y, 1)
     n = a.grid * a.grid // a.gpus
-    entry = {"kernel": a.kernel, "launches_sampled": k, "bytes_fixed": float(c), "bytes_per_projection": float(b),
-             "bytes_per_unknown_per_projection": float(b) / n,
-             "fit_residual_max_rel": float(np.max(np.abs(y - (b * x + c)) / y)),
-             "source": f"{os.path.relpath(a.fetch)} + {os.path.relpath(a.write)} (per launch j = 1..{a.probe_m}, "
-                       "FETCH_SIZE x2 gfx950 correction, linear fit in the projection count 2j; L2<->fabric "
-                       "bytes incl. Infinity-Cache hits)"}
+    entry = {"kernel": a.kernel, "launches_sampled": int(a.probe_m), "bytes_fixed": float(c),
+             "bytes_per_projection": float(b), "bytes_per_unknown_per_projection": float(b) / n,
+             "fit_residual_max_rel": float(np.max(np.abs(y - (b * 2 * js + c)) / y)),
+             "per_step": {str(int(j)): float(v) for j, v in zip(js, y)},
+             "per_step_fused_model_ratio": {str(int(j)): float(v / ((32 * j + 16) * n))
+                                            for j, v in zip(js, y) if j % 16 == 0},
+             "source": f"{os.path.relpath(a.fetch)} + {os.path.relpath(a.write)} (every launch j = 1..{a.probe_m} "
+                       "of one full cycle, FETCH_SIZE x2 gfx950 correction; L2<->fabric bytes incl. "
+                       "Infinity-Cache hits)"}
     db = json.load(open(a.out)) if os.path.exists(a.out) else {}
     db[f"{a.grid}_{a.m}_{a.prec}_{a.method}_{a.gpus}_res"] = entry
     json.dump(db, open(a.out, "w"), indent=1)
-    print(json.dumps(entry, indent=1))
+    print(json.dumps({k: v for k, v in entry.items() if k != "per_step"}, indent=1))
 
 
 def main():
@@ -67,7 +74,7 @@ def main():
     ap.add_argument("--res", action="store_true",
                     help="resident-step kernel (one launch per Arnoldi step j = 1..probe-m in launch order): "
                          "fit bytes per launch = fixed + per_projection * 2j")
-    ap.add_argument("--probe-m", type=int, default=8)
+    ap.add_argument("--probe-m", type=int, default=95, help="resident launches of the traced cycle (= m)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
