@@ -120,7 +120,7 @@ struct gk_ctx {
     i64 xs_words = 0;
     gk::XsPeers xs_peers{};     // every rank's region, mapped here
     std::vector<void *> xs_mapped;
-    bool xs_ready = false, xs_on = false;
+    bool xs_ready = false, xs_on = false, xs_broken = false;
     unsigned xs_seq = 0, xs_hseq = 0;
     int *xs_err = nullptr, *xs_err_dev = nullptr;  // mapped pinned flag
     long long xs_tick_per_ms = 100000;
@@ -237,24 +237,52 @@ int xs_alloc(gk_ctx *c) {
     return GK_OK;
 }
 
-// After a host wait: did a device exchange miss its deadline?
+// The straggler named by a device-side failure code (gk::xs_fail).
+std::string xs_culprit(int code) {
+    const int op = code >> 16, src = (code & 0xFFFF) - 1;
+    char buf[160];
+    switch (op) {
+        case gk::XSE_XCHG: std::snprintf(buf, sizeof buf, "rank %d's all-reduce granule", src); break;
+        case gk::XSE_BCAST: std::snprintf(buf, sizeof buf, "rank %d's broadcast granule", src); break;
+        case gk::XSE_HALO: std::snprintf(buf, sizeof buf, "the halo line of rank %d", src); break;
+        case gk::XSE_RES_WG:
+            std::snprintf(buf, sizeof buf, "workgroup %d of this rank inside a resident step (not co-resident?)", src);
+            break;
+        case gk::XSE_RES_RANK:
+            std::snprintf(buf, sizeof buf, "rank %d's total inside a resident step (rank straggling)", src);
+            break;
+        default: std::snprintf(buf, sizeof buf, "an unknown peer (code %d)", code); break;
+    }
+    return buf;
+}
+
+// After a host wait: did a device exchange miss its deadline?  The exchange is
+// then retired for the life of the context: sequence numbers may differ
+// between ranks after a failed solve (a pipelined step was already queued), so
+// its granules cannot be trusted again -- collectives go to RCCL / the local
+// group (gk_xchg_enable(1) refuses), and resident steps to the launch path.
 int xs_check(gk_ctx *c) {
-    if (c->xs_err != nullptr && __atomic_load_n(c->xs_err, __ATOMIC_ACQUIRE) != 0)
-        return set_err(GK_ERR_COMM, "device exchange: a peer missed the %d ms deadline (rank %d of %d)",
-                       c->xs_timeout_ms, c->rank, c->nranks);
+    const int code = c->xs_err != nullptr ? __atomic_load_n(c->xs_err, __ATOMIC_ACQUIRE) : 0;
+    if (code != 0) {
+        c->xs_broken = true;
+        c->res_broken = true;
+        return set_err(GK_ERR_COMM, "device exchange: rank %d of %d missed the %d ms deadline waiting for %s",
+                       c->rank, c->nranks, c->xs_timeout_ms, xs_culprit(code).c_str());
+    }
     return GK_OK;
 }
 
 // After a host wait: did a resident step miss an in-launch deadline?  Then the
 // context falls back to one launch per projection for the rest of its life.
 int res_check(gk_ctx *c) {
-    if (c->res_err != nullptr && __atomic_load_n(c->res_err, __ATOMIC_ACQUIRE) != 0) {
+    const int code = c->res_err != nullptr ? __atomic_load_n(c->res_err, __ATOMIC_ACQUIRE) : 0;
+    if (code != 0) {
         *c->res_err = 0;
         c->res_broken = true;
         return set_err(GK_ERR_COMM,
-                       "resident MGS-R step: an in-launch exchange missed its %d ms deadline (workgroups not "
-                       "co-resident?); the launch-per-projection path is used from now on",
-                       c->res_timeout_ms);
+                       "resident MGS-R step: an in-launch exchange missed its %d ms deadline waiting for %s; the "
+                       "launch-per-projection path is used from now on",
+                       c->res_timeout_ms, xs_culprit(code).c_str());
     }
     return GK_OK;
 }
@@ -643,13 +671,17 @@ bool res_plan(gk_ctx *c, ResPlan &p) {
     return true;
 }
 
+// hipFuncSetAttribute is per device: remember the dynamic-LDS size set on each.
+constexpr int ATTR_DEVS = 64;
+
 template <int R2, int L2, bool PF, bool NT, bool CW, int MODE>
 int launch_res_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
-    static std::atomic<int> attr{0};
-    if (attr.load() < p.lds) {
+    static std::atomic<int> attr[ATTR_DEVS];
+    if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
+    if (attr[c->dev].load() < p.lds) {
         HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_res<R2, L2, PF, NT, CW, MODE>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
-        attr = p.lds;
+        attr[c->dev] = p.lds;
     }
     gk::k_mgs_res<R2, L2, PF, NT, CW, MODE><<<p.G, gk::RT, p.lds, c->st>>>(a);
     LAUNCHCHK();
@@ -667,11 +699,12 @@ int launch_res_t(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 
 template <int MODE>
 int launch_wres_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
-    static std::atomic<int> attr{0};
-    if (attr.load() < p.lds) {
+    static std::atomic<int> attr[ATTR_DEVS];
+    if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
+    if (attr[c->dev].load() < p.lds) {
         HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RES_RW, RES_LW, MODE>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
-        attr = p.lds;
+        attr[c->dev] = p.lds;
     }
     gk::k_mgs_wres<RES_RW, RES_LW, MODE><<<p.G, gk::WT, p.lds, c->st>>>(a);
     LAUNCHCHK();
@@ -1251,6 +1284,9 @@ int gk_xchg_local(gk_ctx *c) {
 int gk_xchg_enable(gk_ctx *c, int on) {
     if (c == nullptr) return set_err(GK_ERR_ARG, "null context");
     if (on && !c->xs_ready) return set_err(GK_ERR_STATE, "exchange not open");
+    if (on && c->xs_broken)
+        return set_err(GK_ERR_STATE, "device exchange retired after a missed deadline (sequence numbers may "
+                                     "differ between ranks)");
     if (!on && c->comm == nullptr && c->lg == nullptr && c->nranks > 1)
         return set_err(GK_ERR_STATE, "no RCCL or local communicator to fall back to");
     c->xs_on = on != 0;
@@ -1298,7 +1334,7 @@ int xs_selftest_body(gk_ctx *c, std::string &why) {
     if (me < R - 1) HIPCHK(hipMemcpyAsync(hi.data(), c->hhi, sizeof(double) * c->N, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     if (*c->xs_err) {
-        why = "a peer missed the deadline";
+        why = "missed the deadline waiting for " + xs_culprit(*c->xs_err);
         return GK_ERR_COMM;
     }
     for (int k = 0; k < 8; ++k) {

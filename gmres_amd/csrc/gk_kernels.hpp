@@ -818,8 +818,14 @@ __device__ __forceinline__ int xs_flag(const int *err) {
     return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ __forceinline__ void xs_fail(int *err) {
-    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// Which wait missed its deadline (straggler diagnostic, decoded by the host
+// into gk_last_error): code = op << 16 | (source + 1); source = the rank (or,
+// for XSE_RES_WG, the workgroup of this rank) whose granule never came.  A
+// plain store into mapped host memory (no read-modify-write over PCIe): with
+// several failing waits the last one is reported.
+enum { XSE_XCHG = 1, XSE_BCAST = 2, XSE_HALO = 3, XSE_RES_WG = 4, XSE_RES_RANK = 5 };
+__device__ __forceinline__ void xs_fail(int *err, int op, int src) {
+    __hip_atomic_store(err, (op << 16) | ((src + 1) & 0xFFFF), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // All-reduce / broadcast of a short vector, one workgroup per rank.
@@ -863,12 +869,12 @@ __global__ __launch_bounds__(TPB) void k_xchg(double *__restrict__ buf, int coun
             unsigned d = 0;
             ok = xs_get(mine + (((i64)par * XS_MAXR + src) * XS_MAXV + k) * 2 + half, seq, deadline, &d);
             rv[(src * XS_MAXV + k) * 2 + half] = d;
+            if (!ok) xs_fail(err, MODE == XS_BCAST ? XSE_BCAST : XSE_XCHG, src);
         }
         if (!ok) bad = 1;
     }
     __syncthreads();
     if (bad) {
-        if (threadIdx.x == 0) xs_fail(err);
         for (int k = threadIdx.x; k < count; k += TPB) buf[k] = __builtin_nan("");
         return;
     }
@@ -930,7 +936,7 @@ __global__ __launch_bounds__(TPB) void k_xhalo(const double *__restrict__ vec, i
         if (xs_get(q, seq, deadline, &a) && xs_get(q + 1, seq, deadline, &b))
             v = __longlong_as_double((long long)(((u64)b << 32) | a));
         else
-            xs_fail(err);
+            xs_fail(err, XSE_HALO, side == 0 ? rank - 1 : rank + 1);
         (side == 0 ? hlo : hhi)[e] = v;
     }
 }
@@ -1076,6 +1082,16 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
             if (__all(ok)) break;
             if (wall_clock64() > deadline) {
                 all_ok = false;
+                int miss = 0x7FFF;  // the lowest workgroup whose granule never came
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int g = c0 + lane + 64 * k;
+                    if (g < 2 * G && (unsigned)(__hip_atomic_load(slot + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                >> 32) != tag)
+                        miss = min(miss, g >> 1);
+                }
+                for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, 64));
+                if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -1103,6 +1119,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
             const int src = lane >> 1, half = lane & 1;
             ok2 = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV) * 2 + half, seq,
                          wall_clock64() + a.timeout, &d);
+            if (!ok2) xs_fail(a.err, XSE_RES_RANK, src);
         }
         all_ok = __all(ok2);
         double r = 0.0;
@@ -1116,7 +1133,6 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
     if (lane == 0) {
         bc[0] = acc;
         *okf = all_ok ? 1 : 0;
-        if (!all_ok) xs_fail(a.err);
     }
 }
 

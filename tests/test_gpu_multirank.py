@@ -76,7 +76,8 @@ def test_slabs_match_single_context(nranks, method, prec, degree):
     x = np.concatenate([r.x for r in res])
     k = min(len(ref.hist_res), len(res[0].hist_res))
     h, rr = res[0].hist_res[:k], ref.hist_res[:k]
-    tol = np.where(rr > 1e-6, 1e-9, 1e-3 if method == "mgsr" else 0.25)
+    # MGS-R: 1e-3 below r = 1e-6; Householder: the tiers of test_gpu_solver._hist_close_hh
+    tol = np.where(rr > 1e-6, 1e-9, 1e-3 if method == "mgsr" else np.where(rr > 1e-12, 1e-3, 5e-2))
     assert np.all(np.abs(h - rr) <= tol * rr + 1e-16), (h, rr)
     if ref.hist_res[-1] > 1e-6:  # still far from the floor: x itself must agree closely
         assert np.allclose(x, ref.x, rtol=1e-9, atol=1e-12)

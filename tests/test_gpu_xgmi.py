@@ -83,7 +83,8 @@ def _check_against_single(ref, res, method):
         assert np.array_equal(res[0].hist_res, r.hist_res)
     k = min(len(ref.hist_res), len(res[0].hist_res))
     h, rr = res[0].hist_res[:k], ref.hist_res[:k]
-    tol = np.where(rr > 1e-6, 1e-9, 1e-3 if method == "mgsr" else 0.25)
+    # MGS-R: 1e-3 below r = 1e-6; Householder: the tiers of test_gpu_solver._hist_close_hh
+    tol = np.where(rr > 1e-6, 1e-9, 1e-3 if method == "mgsr" else np.where(rr > 1e-12, 1e-3, 5e-2))
     assert np.all(np.abs(h - rr) <= tol * rr + 1e-16), (h, rr)
     x = np.concatenate([r.x for r in res])
     if ref.hist_res[-1] > 1e-6:
@@ -106,6 +107,7 @@ def test_missing_peer_times_out_instead_of_hanging():
     g, ctxs = _local_group(32, 4, 2)
     assert ctxs[0].xchg_selftest(300) is False
     assert "deadline" in ctxs[0].xchg_error
+    assert "rank 1" in ctxs[0].xchg_error  # the straggler is named
     _close(g, ctxs)
 
 
