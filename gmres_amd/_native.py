@@ -13,7 +13,9 @@ import os
 import re
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_DIR = os.path.join(PKG, "lib")
+# GK_LIB_DIR: an A/B build of both libraries (gmres_amd/build.py build_variant);
+# the default is the in-tree build.
+LIB_DIR = os.environ.get("GK_LIB_DIR") or os.path.join(PKG, "lib")
 HIP_SO = os.path.join(LIB_DIR, "libgmres_hip.so")
 FHOST_SO = os.path.join(LIB_DIR, "libgmres_fhost.so")
 HEADER = os.path.join(os.path.dirname(PKG), "include", "gmres_hip.h")
@@ -88,6 +90,7 @@ _SIGS = {
     "gk_profile_reset": (c_int, [c_vp]),
     "gk_profile_read": (c_int, [c_vp, c_int, _dp, ctypes.POINTER(c_ll)]),
     "gk_sync": (c_int, [c_vp]),
+    "gk_profile_res_split": (c_int, [c_vp, c_int, c_int, _dp, _dp, _dp, ctypes.POINTER(c_ll)]),
     "gk_set_tuning": (c_int, [c_vp, c_int, c_int]),
     "gk_lanczos_bounds": (c_int, [c_vp, c_int, _dp, _dp]),
     "gk_vec_count": (c_int, [c_vp, _ip]),

@@ -82,6 +82,21 @@ def build_fortran(force: bool = False) -> str:
     return FHOST_SO
 
 
+def build_variant(name: str, defines: list[str]) -> str:
+    """An A/B build: libgmres_hip.so compiled with extra -D macros (kernel
+    geometry knobs such as GK_RES_RW / GK_RES_WB) plus a copy of the Fortran
+    host beside it (its $ORIGIN rpath then binds that build); select it with
+    GK_LIB_DIR=<returned dir>."""
+    d = os.path.join(LIB, "variants", name)
+    os.makedirs(d, exist_ok=True)
+    so = os.path.join(d, "libgmres_hip.so")
+    _run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+          *[f"-D{x}" for x in defines], *HIP_SOURCES, "-o", so, "-lrccl"])
+    build_fortran()
+    shutil.copy2(FHOST_SO, os.path.join(d, "libgmres_fhost.so"))
+    return d
+
+
 def build_all(force: bool = False) -> None:
     build_hip(force)
     build_fortran(force)

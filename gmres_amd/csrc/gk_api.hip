@@ -138,6 +138,8 @@ struct gk_ctx {
     int res_share = 1;                              // contexts sharing this device's CUs
     int res_timeout_ms = 20000;
     bool res_broken = false;                        // a deadline was missed: launch path from then on
+    gk::u64 *res_stamps = nullptr;                  // gk_profile_res_split: [RGMAX][4] ticks per workgroup
+    bool res_split = false;
     // launch geometry
     int vec = 2, JT = 16;
     dim3 sgrid;
@@ -766,6 +768,7 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
     c->res_tag += (unsigned)np;
     a.timeout = (gk::u64)c->res_timeout_ms * (gk::u64)c->xs_tick_per_ms;
     a.err = c->res_err_dev;
+    a.stamps = c->res_split ? c->res_stamps : nullptr;
     a.nranks = 1;
     if (c->xs_on && c->nranks > 1) {
         a.err = c->xs_err_dev;
@@ -1135,6 +1138,7 @@ int gk_destroy(gk_ctx *c) {
     if (c->xs_buf) (void)hipFree(c->xs_buf);
     if (c->xs_err) (void)hipHostFree(c->xs_err);
     if (c->res_gath) (void)hipFree(c->res_gath);
+    if (c->res_stamps) (void)hipFree(c->res_stamps);
     if (c->res_err) (void)hipHostFree(c->res_err);
     double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi,
                       c->red, c->hcol, c->ydev, c->hb, c->scal, c->Vb, c->gram_slab, c->gram_out};
@@ -1881,6 +1885,50 @@ int gk_profile_read(gk_ctx *c, int kid, double *total_ms, long long *launches) {
     CHK(prof_harvest(c));
     *total_ms = c->prof_ms[kid];
     *launches = c->prof_n[kid];
+    return GK_OK;
+}
+
+int gk_profile_res_split(gk_ctx *c, int mode, int which, double *pass_ms, double *wait_ms, double *total_ms,
+                         long long *launches) {
+    CHK(check_ctx(c));
+    if (which < 0 || which > 2) return set_err(GK_ERR_ARG, "which must be 0 (MGS), 1 (HH up) or 2 (HH down)");
+    HIPCHK(hipSetDevice(c->dev));
+    const size_t bytes = sizeof(gk::u64) * 4 * 3 * gk::RGMAX;
+    if (mode == 1 || mode == 2) {  // enable (and zero) / reset
+        if (c->res_stamps == nullptr) HIPCHK(hipMalloc(&c->res_stamps, bytes));
+        HIPCHK(hipMemsetAsync(c->res_stamps, 0, bytes, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        c->res_split = true;
+    } else if (mode == 0) {
+        c->res_split = false;
+    }
+    if (pass_ms == nullptr || wait_ms == nullptr || total_ms == nullptr || launches == nullptr) return GK_OK;
+    *pass_ms = *wait_ms = *total_ms = 0.0;
+    *launches = 0;
+    if (c->res_stamps == nullptr) return GK_OK;
+    std::vector<gk::u64> h(4 * (size_t)gk::RGMAX);
+    HIPCHK(hipMemcpyAsync(h.data(), c->res_stamps + (size_t)which * 4 * gk::RGMAX, sizeof(gk::u64) * h.size(),
+                          hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    // mean over the workgroups that ran (slot launches > 0), in ms of wall clock
+    double sp = 0, sw = 0, st = 0;
+    int g = 0;
+    long long nl = 0;
+    for (int b = 0; b < gk::RGMAX; ++b)
+        if (h[4 * b + 3] > 0) {
+            sp += (double)h[4 * b];
+            sw += (double)h[4 * b + 1];
+            st += (double)h[4 * b + 2];
+            nl = std::max<long long>(nl, (long long)h[4 * b + 3]);
+            ++g;
+        }
+    if (g > 0) {
+        const double tpm = (double)c->xs_tick_per_ms;
+        *pass_ms = sp / g / tpm;
+        *wait_ms = sw / g / tpm;
+        *total_ms = st / g / tpm;
+    }
+    *launches = nl;
     return GK_OK;
 }
 

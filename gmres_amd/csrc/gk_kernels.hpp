@@ -991,6 +991,40 @@ struct ResArgs {
     int mode;             // RES_MGS / RES_HH_UP / RES_HH_DOWN (res_col)
     double coef;          // AXPY coefficient: w -= (coef*h) V_i (1 for MGS, 2 for reflections)
     i64 tail0;            // RES_HH_UP: the closing norm counts local indices >= tail0
+    u64 *stamps;          // profiling (nullptr = off): [mode][workgroup][pass, wait, total, launches] ticks
+};
+
+// Time split of a resident launch (gk_profile_res_split): thread 0 of each
+// workgroup accumulates wall-clock ticks spent streaming its passes and waiting
+// in the all-gathers into its own slot (no contention, plain adds).
+struct ResClock {
+    u64 t0 = 0, tp = 0, pass = 0, wait = 0;
+    __device__ __forceinline__ void start(const u64 *st) {
+        if (st != nullptr) t0 = tp = wall_clock64();
+    }
+    __device__ __forceinline__ void passed(const u64 *st) {  // a pass ended, its exchange starts
+        if (st != nullptr) {
+            const u64 n = wall_clock64();
+            pass += n - tp;
+            tp = n;
+        }
+    }
+    __device__ __forceinline__ void waited(const u64 *st) {  // the exchange returned
+        if (st != nullptr) {
+            const u64 n = wall_clock64();
+            wait += n - tp;
+            tp = n;
+        }
+    }
+    __device__ __forceinline__ void finish(u64 *st, int mode) {
+        if (st != nullptr && threadIdx.x == 0) {
+            u64 *q = st + 4 * ((i64)mode * RGMAX + blockIdx.x);
+            q[0] += pass;
+            q[1] += wait;
+            q[2] += wall_clock64() - t0;
+            q[3] += 1;
+        }
+    }
 };
 
 // Projection sequences of a resident launch (all columns of V, stride ld):
@@ -1185,6 +1219,8 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
     }
     const i64 sstride = (i64)gridDim.x * DT;
     const i64 sbase = a.nres2 + (i64)blockIdx.x * DT + td;
+    ResClock clk;
+    clk.start(a.stamps);
     int xi = 0;  // exchange index
     double h;
     bool ok = true;
@@ -1334,6 +1370,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
             }
         }
         if (kind == RK_NONE) return true;
+        clk.passed(a.stamps);
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
@@ -1349,6 +1386,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         __syncthreads();
         ++xi;
         h = bc[0];
+        clk.waited(a.stamps);
         return okf != 0;
     };
     if constexpr (PF) {
@@ -1371,6 +1409,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
             }
         }
         if (mode == RES_HH_UP && blockIdx.x == 0 && t == 0) a.hs[0] = h;  // ||w(j+1:n)||^2
+        clk.finish(a.stamps, mode);
         return;
     }
     // h = ||w|| ; V(:,j+1) = w / h  (h == 0: zeros, as k_scale)
@@ -1394,6 +1433,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         }
         if ((a.n & 1) && blockIdx.x == 0 && td == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     }
+    clk.finish(a.stamps, mode);
     if (blockIdx.x == 0) {  // H(1:j+1, j) to the device column and the mapped host mirror
         __syncthreads();
         for (int k = t; k < j; k += RT) {
@@ -1418,7 +1458,19 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
 // Same exchange, same arithmetic as k_mgs_res.
 // --------------------------------------------------------------------------
 constexpr int WT = 256;  // threads per workgroup (4 waves, one per SIMD)
-constexpr int WB = 8;    // double2 per column per batch in flight per thread
+#ifndef GK_RES_WB
+#define GK_RES_WB 8
+#endif
+#ifndef GK_RES_XPF
+#define GK_RES_XPF 0
+#endif
+constexpr int WB = GK_RES_WB;        // double2 per column per batch in flight per thread
+// XPF 1: every wave loads the next pass's first batch before the exchange wait;
+// 2: waves 1..3 only (wave 0 runs the exchange: its polls would queue behind
+// its own prefetch loads, vmcnt retiring in issue order).  Measured: 1 is
+// slower (42.4 -> 46.9 us per projection at RW 80), so the default is 0.
+constexpr int XPF_MODE = GK_RES_XPF;
+constexpr bool XPF = XPF_MODE != 0;
 
 template <int RW, int LW, int MODE>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
@@ -1437,6 +1489,8 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     const i64 tail0 = mode == RES_HH_UP ? a.tail0 : 0;
     const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
     double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
+    ResClock clk;
+    clk.start(a.stamps);
     double2 wr[RW];
 #pragma unroll
     for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < nch) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
@@ -1453,6 +1507,24 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             sq_acc(acc, v, e2, tail0, chk);
         }
     };
+    // XPF: the first batch of a pass (its two columns are known before the dot
+    // that scales it) is loaded before the previous pass's exchange wait, so the
+    // memory pipe is busy while the all-gather completes.
+    double2 pa[WB], pb[WB];
+    const bool xpf_wave = XPF_MODE == 1 || (XPF_MODE == 2 && t >= 64);
+    auto load_first = [&](int i, int q, bool dot) {
+        if (!xpf_wave) return;
+        const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
+        const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
+#pragma unroll
+        for (int u = 0; u < WB; ++u) {
+            const i64 c = c0 + u;
+            if (u < RW && c < nch) {
+                pa[u] = ldv<true>(A2 + c * WT + t);
+                if (dot) pb[u] = B2[c * WT + t];
+            }
+        }
+    };
     // One pass over the slab: w -= ch V_i, then the reduction `kind`
     // (<w, V_q>, ||w(tail0:)||^2, or none).  Returns this thread's partial.
     auto pass = [&](double ch, int i, int q, int kind) -> double {
@@ -1467,7 +1539,10 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
                 const i64 c = c0 + k0 + u;
-                if (k0 + u < RW && c < nch) {
+                if (XPF && k0 == 0 && xpf_wave) {
+                    av[u] = pa[u];
+                    bv[u] = pb[u];
+                } else if (k0 + u < RW && c < nch) {
                     av[u] = ldv<true>(A2 + c * WT + t);
                     if (dot) bv[u] = B2[c * WT + t];
                 }
@@ -1539,6 +1614,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     // all-gather of the partials: the same h in every workgroup (and rank)
     int xi = 0;
     auto reduce = [&](double acc, double &h) -> bool {
+        clk.passed(a.stamps);
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
@@ -1546,16 +1622,22 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         __syncthreads();
         ++xi;
         h = bc[0];
+        clk.waited(a.stamps);
         return okf != 0;
     };
+    auto kind_of = [&](int p) { return p < np - 1 ? RK_DOT : (mode == RES_HH_DOWN ? RK_NONE : RK_NORM); };
     double h;
     bool ok = true;
     if (mode == RES_HH_DOWN) {
         // the pre-dot as an AXPY pass with h = 0 (w - 0 V = w): a dot-only copy of the
         // unrolled register loop would not fit the register file
         const int q = res_col(mode, j, 0);
-        ok = reduce(pass(0.0, q, q, RK_DOT), h);
+        if (XPF) load_first(q, q, true);
+        const double acc = pass(0.0, q, q, RK_DOT);
+        if (XPF) load_first(q, res_col(mode, j, 1), kind_of(0) == RK_DOT);
+        ok = reduce(acc, h);
     } else {
+        if (XPF) load_first(res_col(mode, j, 0), res_col(mode, j, 1), kind_of(0) == RK_DOT);
         double s = 0.0;
         for (int k = t; k < a.npin; k += WT) s += a.pin[k];
         s = wave_sum(s);
@@ -1568,10 +1650,10 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     }
     for (int p = 0; p < np && ok; ++p) {
         const int i = res_col(mode, j, p);
-        const bool last = p == np - 1;
-        const int kind = !last ? RK_DOT : (mode == RES_HH_DOWN ? RK_NONE : RK_NORM);
+        const int kind = kind_of(p);
         if (mode == RES_MGS && blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
         const double acc = pass(mode == RES_MGS ? h : a.coef * h, i, res_col(mode, j, p + 1), kind);
+        if (XPF && p + 1 < np) load_first(res_col(mode, j, p + 1), res_col(mode, j, p + 2), kind_of(p + 1) == RK_DOT);
         if (kind != RK_NONE) ok = reduce(acc, h);
     }
     if (!ok) return;  // uniform per workgroup; *err is set
@@ -1582,6 +1664,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         for (int k = 0; k < LW; ++k)
             if (l0 + k < nch) W2[(l0 + k) * WT + t] = lw[k * WT + t];
         if (mode == RES_HH_UP && blockIdx.x == 0 && t == 0) a.hs[0] = h;  // ||w(j+1:n)||^2
+        clk.finish(a.stamps, mode);
         return;
     }
     const double hn = sqrt(h);
@@ -1600,6 +1683,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
     }
     if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
+    clk.finish(a.stamps, mode);
     if (blockIdx.x == 0) {
         __syncthreads();
         for (int k = t; k < j; k += WT) {

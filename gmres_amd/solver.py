@@ -259,6 +259,16 @@ class Context:
             out[name] = (ms.value, int(n.value))
         return out
 
+    def res_split(self, mode: int = -1, which: int = 0) -> dict:
+        """In-launch time split of the resident launches (gk_profile_res_split):
+        mode 1 enable + zero, 2 zero, 0 disable, -1 read only; which 0 MGS-R
+        steps, 1 Householder UP chains, 2 Householder DOWN chains."""
+        p, w, t = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = nat.c_ll()
+        nat.check(nat.hip().gk_profile_res_split(self._h, int(mode), int(which), ctypes.byref(p), ctypes.byref(w),
+                                                 ctypes.byref(t), ctypes.byref(n)), "gk_profile_res_split")
+        return {"pass_ms": p.value, "wait_ms": w.value, "total_ms": t.value, "launches": int(n.value)}
+
     def tune(self, key: int, value: int) -> None:
         """Launch-policy knob (include/gmres_hip.h GK_TUNE_*)."""
         nat.check(nat.hip().gk_set_tuning(self._h, int(key), int(value)), "gk_set_tuning")

@@ -211,6 +211,15 @@ int gk_vec_lincomb(gk_ctx *ctx, int form, int out, int a, int b, int c, double s
 int gk_profile_enable(gk_ctx *ctx, int enable);
 int gk_profile_reset(gk_ctx *ctx);
 int gk_profile_read(gk_ctx *ctx, int kid, double *total_ms, long long *launches);
+/* Time split of the resident launches, measured inside them (wall clock of
+ * thread 0 of every workgroup): mode 1 enables and zeroes, 2 zeroes, 0
+ * disables, -1 only reads.  For the launches of kind `which` (0 MGS-R step,
+ * 1 Householder UP chain, 2 Householder DOWN chain) since the last reset:
+ * the mean over workgroups of the time streaming passes, the time waiting in
+ * the in-launch all-gathers, and the launch total, summed over launches (out
+ * pointers may be NULL to skip reading). */
+int gk_profile_res_split(gk_ctx *ctx, int mode, int which, double *pass_ms, double *wait_ms, double *total_ms,
+                         long long *launches);
 int gk_sync(gk_ctx *ctx);
 
 /* Launch-policy knobs (defaults are the tuned values; for A/B measurement).
