@@ -91,6 +91,7 @@ struct gk_ctx {
     double *V = nullptr;  // (m+1) columns, stride ld
     double *w = nullptr, *z = nullptr, *aux = nullptr, *dA = nullptr, *dB = nullptr;
     double *x = nullptr, *b = nullptr, *vj = nullptr, *hlo = nullptr, *hhi = nullptr;
+    double *dh = nullptr;  // deep halos of the Chebyshev pass inputs: [3 vectors][lo, hi][CF_LMAX lines][N]
     double *red = nullptr;   // NSLOT * NPMAX partial slabs
     double *hcol = nullptr;  // m+2 Hessenberg column / scalars
     double *ydev = nullptr;  // m+1
@@ -223,7 +224,7 @@ void xs_set_timeout(gk_ctx *c, int ms) {
 int xs_alloc(gk_ctx *c) {
     if (c->xs_buf != nullptr) return GK_OK;
     HIPCHK(hipSetDevice(c->dev));
-    c->xs_words = gk::XS_RED_WORDS + 8LL * c->N;
+    c->xs_words = gk::XS_RED_WORDS + 8LL * gk::XS_HALO_LINES * c->N;
     if (hipExtMallocWithFlags((void **)&c->xs_buf, sizeof(gk::u64) * c->xs_words, hipDeviceMallocUncached) !=
         hipSuccess)
         return set_err(GK_ERR_NOMEM, "cannot allocate the exchange region");
@@ -402,29 +403,32 @@ int bcast(gk_ctx *c, double *buf, int count, int root) {
     return GK_OK;
 }
 
-// Exchange the first / last local grid line of vec with the slab neighbours.
-int halo(gk_ctx *c, const double *vec) {
+// Exchange nl grid lines of vec with the slab neighbours: lo <- the last nl
+// lines of rank-1 (our rows -nl..-1), hi <- the first nl lines of rank+1 (our
+// rows nlines..nlines+nl-1).  nl = 1 for a stencil sweep; the temporal-blocked
+// Chebyshev passes need nl = L (their recompute cone).
+int halo_lines(gk_ctx *c, const double *vec, int nl, double *lo, double *hi) {
     if (!collective(c)) return GK_OK;
     ProfScope ps(c, GK_KID_COMM);
     const int N = c->N;
+    const i64 cnt = (i64)nl * N;
     if (c->xs_on) {
         if (c->nranks == 1) return GK_OK;
         const unsigned seq = ++c->xs_hseq;
-        gk::k_xhalo<<<(N + gk::TPB - 1) / gk::TPB, gk::TPB, 0, c->st>>>(vec, N, c->nlines, c->xs_peers, c->nranks,
-                                                                       c->rank, seq, c->hlo, c->hhi, c->xs_err_dev,
-                                                                       c->xs_timeout);
+        gk::k_xhalo<<<(unsigned)((cnt + gk::TPB - 1) / gk::TPB), gk::TPB, 0, c->st>>>(
+            vec, N, c->nlines, nl, c->xs_peers, c->nranks, c->rank, seq, lo, hi, c->xs_err_dev, c->xs_timeout);
         LAUNCHCHK();
         return GK_OK;
     }
     if (c->lg == nullptr) {
         NCCLCHK(ncclGroupStart());
         if (c->rank > 0) {
-            NCCLCHK(ncclSend(vec, N, ncclDouble, c->rank - 1, c->comm, c->st));
-            NCCLCHK(ncclRecv(c->hlo, N, ncclDouble, c->rank - 1, c->comm, c->st));
+            NCCLCHK(ncclSend(vec, cnt, ncclDouble, c->rank - 1, c->comm, c->st));
+            NCCLCHK(ncclRecv(lo, cnt, ncclDouble, c->rank - 1, c->comm, c->st));
         }
         if (c->rank < c->nranks - 1) {
-            NCCLCHK(ncclSend(vec + (i64)(c->nlines - 1) * N, N, ncclDouble, c->rank + 1, c->comm, c->st));
-            NCCLCHK(ncclRecv(c->hhi, N, ncclDouble, c->rank + 1, c->comm, c->st));
+            NCCLCHK(ncclSend(vec + (i64)(c->nlines - nl) * N, cnt, ncclDouble, c->rank + 1, c->comm, c->st));
+            NCCLCHK(ncclRecv(hi, cnt, ncclDouble, c->rank + 1, c->comm, c->st));
         }
         NCCLCHK(ncclGroupEnd());
         return GK_OK;
@@ -433,12 +437,12 @@ int halo(gk_ctx *c, const double *vec) {
     if (c->rank > 0) {
         gk_ctx *o = c->lg->members[c->rank - 1];
         CHK(lg_wait(c, c->rank - 1, false));
-        HIPCHK(hipMemcpyAsync(c->hlo, c->lg->ptrs[c->rank - 1] + (i64)(o->nlines - 1) * N, sizeof(double) * N,
+        HIPCHK(hipMemcpyAsync(lo, c->lg->ptrs[c->rank - 1] + (i64)(o->nlines - nl) * N, sizeof(double) * cnt,
                               hipMemcpyDeviceToDevice, c->st));
     }
     if (c->rank < c->nranks - 1) {
         CHK(lg_wait(c, c->rank + 1, false));
-        HIPCHK(hipMemcpyAsync(c->hhi, c->lg->ptrs[c->rank + 1], sizeof(double) * N, hipMemcpyDeviceToDevice, c->st));
+        HIPCHK(hipMemcpyAsync(hi, c->lg->ptrs[c->rank + 1], sizeof(double) * cnt, hipMemcpyDeviceToDevice, c->st));
     }
     HIPCHK(hipEventRecord(c->lev_b, c->st));
     CHK(lg_barrier(c));
@@ -446,6 +450,8 @@ int halo(gk_ctx *c, const double *vec) {
     if (c->rank < c->nranks - 1) CHK(lg_wait(c, c->rank + 1, true));
     return GK_OK;
 }
+
+int halo(gk_ctx *c, const double *vec) { return halo_lines(c, vec, 1, c->hlo, c->hhi); }
 
 const double *halo_lo(gk_ctx *c) { return (c->nranks > 1 && c->rank > 0) ? c->hlo : nullptr; }
 const double *halo_hi(gk_ctx *c) { return (c->nranks > 1 && c->rank < c->nranks - 1) ? c->hhi : nullptr; }
@@ -852,6 +858,17 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
         }
         return dim3(gx, gy, 1);
     };
+    // On slabs every input of a pass brings L lines of each neighbour (deep halo).
+    const bool slabs = collective(c) && c->nranks > 1;
+    const bool has_lo = slabs && c->rank > 0, has_hi = slabs && c->rank < c->nranks - 1;
+    auto dlo = [&](int v) { return c->dh + (i64)(2 * v) * gk::CF_LMAX * c->N; };
+    auto dhi = [&](int v) { return c->dh + (i64)(2 * v + 1) * gk::CF_LMAX * c->N; };
+    auto deep = [&](gk::CFArgs &x, int v, const double *vec, int L) -> int {
+        if (slabs) CHK(halo_lines(c, vec, L, dlo(v), dhi(v)));
+        x.lo[v] = has_lo ? dlo(v) : nullptr;
+        x.hi[v] = has_hi ? dhi(v) : nullptr;
+        return GK_OK;
+    };
     gk::CFArgs a{};
     a.N = c->N;
     a.nlines = c->nlines;
@@ -859,6 +876,7 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
     a.din = c->z;
     a.vdot = vdot;
     a.part = part;
+    CHK(deep(a, 0, c->z, g1));
     for (int l = 0; l < g1; ++l) {
         a.c1[l] = c1[l];
         a.c2[l] = c2[l];
@@ -881,6 +899,9 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
     b.din = c->dA;
     b.rin = c->aux;
     b.zin = c->dB;
+    CHK(deep(b, 0, c->dA, g2));
+    CHK(deep(b, 1, c->aux, g2));
+    CHK(deep(b, 2, c->dB, g2));
     b.out = out;
     b.vdot = vdot;
     b.part = part;
@@ -894,9 +915,18 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
     return launch_cf<false, true>(c, g2, g, acc, b);
 }
 
+// Temporal-blocked Chebyshev passes: even N (two points per lane), k <= 8,
+// and on slabs every rank holding at least CF_LMAX lines (the deep halo).
+bool cheb_fused_ok(gk_ctx *c) {
+    if (!c->tune_cheb_fused || c->N % 2 != 0 || c->pdeg > 2 * gk::CF_LMAX) return false;
+    if (!collective(c) || c->nranks == 1) return true;
+    return c->N / c->nranks >= gk::CF_LMAX;  // the smallest slab of slab_partition
+}
+
 // out = M^-1 z for z already in c->z (cbpr2 or Chebyshev sweeps).
 int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *part) {
-    CHK(halo(c, c->z));
+    const bool fused = c->pkind == GK_PREC_CHEB && cheb_fused_ok(c);
+    if (!fused) CHK(halo(c, c->z));  // the fused passes bring their own deep halos
     if (c->pkind == GK_PREC_CBPR2) {
         // cbpr2 coefficients exactly as chebyshev.f90:19-25
         const double em = c->p0, eM = c->p1;
@@ -921,7 +951,7 @@ int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *
     const double delta = std::fabs(c->p1 - c->p0) / 2.0;
     const double sigma = theta / delta;
     double rho0 = delta / theta;
-    if (c->tune_cheb_fused && !collective(c) && c->N % 2 == 0 && c->pdeg <= 2 * gk::CF_LMAX) {
+    if (fused) {
         double c1[2 * gk::CF_LMAX], c2[2 * gk::CF_LMAX];
         for (int it = 0; it < c->pdeg; ++it) {
             const double rho1 = 1.0 / (2.0 * sigma - rho0);
@@ -1082,6 +1112,7 @@ int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out)
         if (hipMalloc(p, vb) != hipSuccess) return fail(set_err(GK_ERR_NOMEM, "cannot allocate work vectors"));
     if (hipMalloc(&c->hlo, sizeof(double) * nside) != hipSuccess ||
         hipMalloc(&c->hhi, sizeof(double) * nside) != hipSuccess ||
+        hipMalloc(&c->dh, sizeof(double) * 6 * gk::CF_LMAX * (size_t)nside) != hipSuccess ||
         hipMalloc(&c->red, sizeof(double) * NSLOT * gk::NPMAX) != hipSuccess ||
         hipMalloc(&c->hcol, sizeof(double) * (m + 2)) != hipSuccess ||
         hipMalloc(&c->ydev, sizeof(double) * (m + 1)) != hipSuccess ||
@@ -1140,7 +1171,7 @@ int gk_destroy(gk_ctx *c) {
     if (c->res_gath) (void)hipFree(c->res_gath);
     if (c->res_stamps) (void)hipFree(c->res_stamps);
     if (c->res_err) (void)hipHostFree(c->res_err);
-    double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi,
+    double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi, c->dh,
                       c->red, c->hcol, c->ydev, c->hb, c->scal, c->Vb, c->gram_slab, c->gram_out};
     for (double *p : bufs)
         if (p) (void)hipFree(p);

@@ -640,6 +640,10 @@ struct CFArgs {
     double theta;        // FIRST: d0 = r / theta
     double c1[CF_LMAX], c2[CF_LMAX];
     int N, nlines, JT;
+    // Row-block slabs (deep halo): L grid lines of each input from the slab
+    // neighbours -- lo[*] = rows -L..-1, hi[*] = rows nlines..nlines+L-1 --
+    // or nullptr at the physical boundary.  Index 0: din, 1: rin, 2: zin.
+    const double *lo[3], *hi[3];
 };
 
 template <int L, bool FIRST, bool LAST, int ACC>
@@ -664,10 +668,20 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
             dw[l][0][k] = dw[l][1][k] = dw[l][2][k] = 0.0;
             rm[l][k] = zm[l][k] = rn[l][k] = zn[l][k] = 0.0;
         }
-    auto ld2 = [&](const double *base, int row, double (&v)[2]) {
+    // rows of the slab, or of a neighbour's deep halo (rows -L.. / nlines..)
+    const bool has_lo = a.lo[0] != nullptr, has_hi = a.hi[0] != nullptr;
+    auto ld2 = [&](int which, const double *base, int row, double (&v)[2]) {
         v[0] = v[1] = 0.0;
-        if (row < 0 || row >= a.nlines) return;
-        const double *p = base + (i64)row * N + i0;
+        const double *p;
+        if (row < 0) {
+            if (!has_lo || row < -L) return;
+            p = a.lo[which] + (i64)(row + L) * N + i0;
+        } else if (row >= a.nlines) {
+            if (!has_hi || row >= a.nlines + L) return;
+            p = a.hi[which] + (i64)(row - a.nlines) * N + i0;
+        } else {
+            p = base + (i64)row * N + i0;
+        }
         if (in0 && in1) {
             const double2 t = *reinterpret_cast<const double2 *>(p);
             v[0] = t.x;
@@ -676,10 +690,10 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
     };
     // input line t+1 is in flight while line t runs through the levels
     auto ld_in = [&](int row, double (&d)[2], double (&r)[2], double (&z)[2]) {
-        ld2(a.din, row, d);
+        ld2(0, a.din, row, d);
         if (!FIRST) {
-            ld2(a.rin, row, r);
-            ld2(a.zin, row, z);
+            ld2(1, a.rin, row, r);
+            ld2(2, a.zin, row, z);
         }
     };
     if (j0 < a.nlines) {
@@ -726,7 +740,10 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
                 const int mrow = row - 1;
                 double left = __shfl_up(dw[l][1][1], 1, 64);
                 double right = __shfl_down(dw[l][1][0], 1, 64);
-                const bool rowok = mrow >= 0 && mrow < a.nlines;
+                // a row outside the GRID is zero at every level (rows in a
+                // neighbour's halo are real; the deepest ones are wrong but
+                // never reach the kept rows -- the usual L-row recompute cone)
+                const bool rowok = (has_lo || mrow >= 0) && (has_hi || mrow < a.nlines);
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const double W = (k == 0) ? left : dw[l][1][0];
@@ -901,14 +918,20 @@ __global__ __launch_bounds__(TPB) void k_xchg(double *__restrict__ buf, int coun
 // Halo lines through the same regions: my first grid line goes to rank-1
 // (its side 1), my last to rank+1 (its side 0); then wait for mine and decode
 // them into hlo / hhi, the buffers the stencil reads.  One thread per point.
-__global__ __launch_bounds__(TPB) void k_xhalo(const double *__restrict__ vec, int N, int nlines, XsPeers peers,
-                                               int nranks, int rank, unsigned seq, double *__restrict__ hlo,
-                                               double *__restrict__ hhi, int *err, u64 timeout) {
-    const int e = blockIdx.x * TPB + threadIdx.x;
-    if (e >= N) return;
+constexpr int XS_HALO_LINES = CF_LMAX;  // deepest halo (the temporal-blocked Chebyshev passes)
+
+__global__ __launch_bounds__(TPB) void k_xhalo(const double *__restrict__ vec, int N, int nlines, int nl,
+                                               XsPeers peers, int nranks, int rank, unsigned seq,
+                                               double *__restrict__ hlo, double *__restrict__ hhi, int *err,
+                                               u64 timeout) {
+    // nl grid lines each way: my first nl lines go to rank-1, my last nl to rank+1
+    const i64 e = (i64)blockIdx.x * TPB + threadIdx.x;
+    if (e >= (i64)nl * N) return;
     const bool lo = rank > 0, hi = rank < nranks - 1;
     const unsigned par = seq & 1u;
-    auto slot = [&](u64 *base, int side) { return base + gk::XS_RED_WORDS + (((i64)par * 2 + side) * N + e) * 2; };
+    auto slot = [&](u64 *base, int side) {
+        return base + gk::XS_RED_WORDS + (((i64)par * 2 + side) * ((i64)XS_HALO_LINES * N) + e) * 2;
+    };
     if (xs_flag(err)) {
         if (lo) hlo[e] = __builtin_nan("");
         if (hi) hhi[e] = __builtin_nan("");
@@ -921,7 +944,7 @@ __global__ __launch_bounds__(TPB) void k_xhalo(const double *__restrict__ vec, i
         xs_put(q + 1, seq, (unsigned)(bits >> 32));
     }
     if (hi) {
-        const u64 bits = (u64)__double_as_longlong(vec[(i64)(nlines - 1) * N + e]);
+        const u64 bits = (u64)__double_as_longlong(vec[(i64)(nlines - nl) * N + e]);
         u64 *q = slot(peers.p[rank + 1], 0);
         xs_put(q, seq, (unsigned)bits);
         xs_put(q + 1, seq, (unsigned)(bits >> 32));

@@ -143,3 +143,39 @@ def test_rccl_one_rank_communicator(monkeypatch, method, prec):
         r = _solve(c, method, prec, 4)
     assert np.array_equal(r.hist_res, ref.hist_res)
     assert np.array_equal(r.x, ref.x)
+
+
+@pytest.mark.parametrize("N,nranks", [(66, 3), (20, 4), (16, 5), (130, 2)])
+@pytest.mark.parametrize("degree", [1, 3, 4, 6, 8])
+def test_chebyshev_on_slabs_bitexact(oracle, N, nranks, degree):
+    """M^-1 r on row-block slabs: the temporal-blocked Chebyshev passes take
+    a deep halo (L lines of every pass input from each neighbour) and give the
+    single-grid result bit for bit; slabs thinner than 4 lines (16 / 5) take
+    the per-sweep kernels, also bit-exact."""
+    import gmres_amd as ga
+
+    r = np.random.default_rng(N + degree).standard_normal(N * N)
+    ref = oracle.precond(oracle.PREC_CHEB, r, N, params=(8.2, 0.2), degree=degree)
+    parts = ga.slab_partition(N, nranks)
+    g = ga.LocalGroup(nranks)
+    ctxs = [ga.Context(N, 8, line0=l0, nlines=nl) for l0, nl in parts]
+    out = [None] * nranks
+    try:
+        for q, c in enumerate(ctxs):
+            c.comm_init_local(g, q, max(nl for _, nl in parts))
+            c.set_precond("cheb", (8.2, 0.2), degree)
+
+        def work(q):
+            l0, nl = parts[q]
+            out[q] = ctxs[q].apply(r[l0 * N:(l0 + nl) * N], 1)
+
+        th = [threading.Thread(target=work, args=(q,)) for q in range(nranks)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=60)
+        assert np.array_equal(np.concatenate(out), ref)
+    finally:
+        for c in ctxs:
+            c.close()
+        g.close()

@@ -245,3 +245,20 @@ def test_processes_share_regions_by_ipc(nranks, force_res):
     k = min(len(ref.hist_res), len(res[0][1]))
     assert np.allclose(res[0][1][:k], ref.hist_res[:k], rtol=1e-9, atol=1e-16)
     assert np.allclose(x, ref.x, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("N,nranks,degree", [(66, 3, 8), (40, 2, 5), (20, 4, 4)])
+def test_chebyshev_deep_halo_over_device_exchange(oracle, N, nranks, degree):
+    """The deep halo of the temporal-blocked Chebyshev passes through the
+    device exchange (k_xhalo with L lines): bit-exact against the oracle."""
+    r = np.random.default_rng(N * degree).standard_normal(N * N)
+    ref = oracle.precond(oracle.PREC_CHEB, r, N, params=(8.2, 0.2), degree=degree)
+    import gmres_amd as ga
+
+    g, ctxs = _local_group(N, 8, nranks)
+    parts = ga.slab_partition(N, nranks)
+    for c in ctxs:
+        c.set_precond("cheb", (8.2, 0.2), degree)
+    out = _run_threads(nranks, lambda q: ctxs[q].apply(r[parts[q][0] * N:(parts[q][0] + parts[q][1]) * N], 1))
+    _close(g, ctxs)
+    assert np.array_equal(np.concatenate(out), ref)
