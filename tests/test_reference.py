@@ -81,13 +81,15 @@ def test_oracle_1024_serial_three_cycles_bit_exact(oracle):
         assert np.array_equal(r.hist_res, np.array(REF[k]["hist_res"])), (k, r.hist_res, REF[k]["hist_res"])
 
 
-@pytest.mark.parametrize("key,rtol", [("hh_omp_identity_1024_m95_3cyc_t8", 5e-11),
+@pytest.mark.parametrize("key,rtol", [("hh_omp_identity_1024_m95_3cyc_t8", 1e-10),
                                       ("mgsr_omp_identity_1024_m95_3cyc_t8", 1e-12)])
 def test_oracle_1024_threaded_vs_reference(oracle, key, rtol):
     """8 OpenMP threads on both sides (libomp vs libgomp reduction trees):
     per-cycle residuals within 1e-12 relative for MGS-R (measured 4e-13) and
-    5e-11 for Householder (measured 1.4e-11 at cycle 3 -- the reference's own
-    HH and MGS-R runs differ by 1.6e-11 there)."""
+    1e-10 for Householder (measured 1.4e-11 .. 4.4e-11 at cycle 3 over repeated
+    8-thread runs: the threaded reductions are not run-to-run deterministic on
+    either side, and the reference's own HH and MGS-R runs differ by 1.6e-11
+    there)."""
     g = REF[key]
     r = _oracle_run(oracle, g, threads=8, max_cycles=3)
     assert np.allclose(r.hist_res, g["hist_res"], rtol=rtol, atol=0)
