@@ -24,6 +24,7 @@ GK_OK = 0
 GK_ERR_COMM = -6
 GK_TUNE_XCHG_TIMEOUT_MS = 7
 GK_TUNE_RES, GK_TUNE_RES_R2, GK_TUNE_RES_SHARE, GK_TUNE_RES_TIMEOUT_MS = 8, 9, 10, 11
+GK_TUNE_VERR_ORDER = 14
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES = range(7)
 KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res"]
@@ -71,6 +72,7 @@ _SIGS = {
     "gk_rhs_norm": (c_int, [c_vp, _dp]),
     "gk_zero_x": (c_int, [c_vp]),
     "gk_get_x": (c_int, [c_vp, _dp]),
+    "gk_get_basis": (c_int, [c_vp, c_int, c_int, _dp]),
     "gk_set_x": (c_int, [c_vp, _dp]),
     "gk_apply": (c_int, [c_vp, c_int, _dp, _dp]),
     "gk_true_residual": (c_int, [c_vp, _dp]),

@@ -136,6 +136,7 @@ struct gk_ctx {
     int tune_res_r2 = 0;                            // cap of resident double2 per thread (0 = auto)
     int tune_res_lds = 1;                           // LDS-resident part of w for large slabs
     int tune_res_wonly = -1;                        // large slabs: w-only variant (-1: by the byte model)
+    int tune_verr_order = 1;                        // v_err diagnostics in the reference's dot order
     int res_share = 1;                              // contexts sharing this device's CUs
     int res_timeout_ms = 20000;
     bool res_broken = false;                        // a deadline was missed: launch path from then on
@@ -1007,6 +1008,11 @@ int check_ctx(gk_ctx *c) {
     return GK_OK;
 }
 
+// The orthogonality diagnostics in the reference's summation order (one running
+// sum per dot, gk::seq_dot) unless tuned off; a running sum cannot cross a slab
+// boundary without serialising the ranks, so N ranks use the tree (k_gram).
+bool verr_ref_order(const gk_ctx *c) { return c->tune_verr_order != 0 && c->nranks == 1; }
+
 int ensure_gram(gk_ctx *c, int ncols) {
     if (ncols > gk::GCMAX) return set_err(GK_ERR_ARG, "v_err needs <= %d columns", gk::GCMAX);
     if (c->gram_slab == nullptr) {
@@ -1027,7 +1033,11 @@ int gram(gk_ctx *c, const double *base, int ncols, std::vector<double> &G) {
         for (int aa = 0; aa <= bb; ++aa) pr.push_back(make_short2((short)aa, (short)bb));
     const int np = (int)pr.size();
     HIPCHK(hipMemcpyAsync(c->gram_pairs, pr.data(), sizeof(short2) * np, hipMemcpyHostToDevice, c->st));
-    {
+    if (verr_ref_order(c)) {  // one running sum per pair, k in order (the reference's dot_product)
+        ProfScope ps(c, GK_KID_OTHER);
+        gk::k_seqdot_pairs<<<(np + 63) / 64, 64, 0, c->st>>>(base, c->ld, c->nloc, c->gram_pairs, np, c->gram_out);
+        LAUNCHCHK();
+    } else {
         ProfScope ps(c, GK_KID_OTHER);
         gk::k_gram<<<c->gram_nblk, gk::TPB, 0, c->st>>>(base, c->ld, ncols, c->nloc, c->gram_pairs, np,
                                                         c->gram_slab);
@@ -1035,8 +1045,8 @@ int gram(gk_ctx *c, const double *base, int ncols, std::vector<double> &G) {
         gk::k_gram_reduce<<<(np + gk::TPB - 1) / gk::TPB, gk::TPB, 0, c->st>>>(c->gram_slab, c->gram_nblk,
                                                                             np, c->gram_out);
         LAUNCHCHK();
+        CHK(allreduce(c, c->gram_out, np, true));
     }
-    CHK(allreduce(c, c->gram_out, np, true));
     std::vector<double> flat(np);
     HIPCHK(hipMemcpyAsync(flat.data(), c->gram_out, sizeof(double) * np, hipMemcpyDeviceToHost, c->st));
     CHK(sync_st(c));
@@ -1504,6 +1514,18 @@ int gk_get_x(gk_ctx *c, double *x) {
     return GK_OK;
 }
 
+int gk_get_basis(gk_ctx *c, int which, int col, double *out) {
+    CHK(check_ctx(c));
+    const double *base = which == 0 ? c->V : (which == 1 ? c->Vb : nullptr);
+    const int ncol = which == 0 ? c->m + 1 : c->m;
+    if (base == nullptr) return set_err(GK_ERR_ARG, "basis %d not available", which);
+    if (col < 0 || col >= ncol) return set_err(GK_ERR_ARG, "bad column %d", col);
+    HIPCHK(hipSetDevice(c->dev));
+    HIPCHK(hipMemcpyAsync(out, base + (i64)col * c->ld, sizeof(double) * c->nloc, hipMemcpyDeviceToHost, c->st));
+    CHK(sync_st(c));
+    return GK_OK;
+}
+
 int gk_set_x(gk_ctx *c, const double *x) {
     CHK(check_ctx(c));
     HIPCHK(hipSetDevice(c->dev));
@@ -1807,7 +1829,19 @@ int gk_hh_verr(gk_ctx *c, int n_out, double *v_err) {
         double *col = c->Vb + (i64)(i - 1) * c->ld;
         gk::k_set_unit<<<c->nblk_stream, gk::TPB, 0, c->st>>>(col, c->nloc, c->g0, i - 1, 1.0);
         LAUNCHCHK();
-        CHK(reflect_chain_down(c, col, i));
+        if (!verr_ref_order(c)) CHK(reflect_chain_down(c, col, i));
+    }
+    if (verr_ref_order(c)) {  // :581-585 with the reference's dots, all chains level by level
+        CHK(ensure_gram(c, n_out));
+        ProfScope ps(c, GK_KID_OTHER);
+        for (int s = 0; s < n_out; ++s) {
+            gk::k_hh_rebuild_dot<<<(n_out - s + 63) / 64, 64, 0, c->st>>>(c->Vb, c->V, c->ld, c->nloc, s, n_out,
+                                                                          c->gram_out);
+            LAUNCHCHK();
+            gk::k_hh_rebuild_upd<<<dim3(c->nblk_stream, n_out - s), gk::TPB, 0, c->st>>>(c->Vb, c->V, c->ld,
+                                                                                       c->nloc, s, c->gram_out);
+            LAUNCHCHK();
+        }
     }
     std::vector<double> G;
     CHK(gram(c, c->Vb, n_out, G));
@@ -1874,6 +1908,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
             break;
         case GK_TUNE_RES_LDS: c->tune_res_lds = value != 0; break;
         case GK_TUNE_RES_WONLY: c->tune_res_wonly = value < 0 ? -1 : (value != 0); break;
+        case GK_TUNE_VERR_ORDER: c->tune_verr_order = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
             c->res_timeout_ms = value;

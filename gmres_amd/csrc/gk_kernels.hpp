@@ -609,6 +609,71 @@ __global__ __launch_bounds__(TPB) void k_gram_reduce(const double *__restrict__ 
     out[p] = s;
 }
 
+// --------------------------------------------------------------------------
+// Reference-order dots for the orthogonality diagnostics (gmres_mgsr.f90:414-420,
+// gmres_hh.f90:568-593).  Fortran dot_product is ONE running sum
+// h = h + a(k)*b(k), k = 1..n.  Both diagnostics measure rounding noise, and
+// the reference's figure is dominated by that running sum's own rounding, so
+// the device evaluates them the same way: one lane per dot, k in order,
+// multiply then add (-ffp-contract=off) -- bit-identical to the reference's
+// formula on the same basis.  n dependent adds per lane: slow by design, run
+// once per solve (the tree-reduced k_gram is the fast alternative).
+// --------------------------------------------------------------------------
+constexpr int SQ_B = 8;  // double2 per column in flight per lane
+
+__device__ __forceinline__ double seq_dot(const double *__restrict__ a, const double *__restrict__ b, i64 n) {
+    const double2 *a2 = reinterpret_cast<const double2 *>(a), *b2 = reinterpret_cast<const double2 *>(b);
+    const i64 n2 = n >> 1;
+    double h = 0.0;
+    i64 e = 0;
+    for (; e + SQ_B <= n2; e += SQ_B) {
+        double2 x[SQ_B], y[SQ_B];
+#pragma unroll
+        for (int u = 0; u < SQ_B; ++u) {
+            x[u] = a2[e + u];
+            y[u] = b2[e + u];
+        }
+#pragma unroll
+        for (int u = 0; u < SQ_B; ++u) {
+            h = h + x[u].x * y[u].x;
+            h = h + x[u].y * y[u].y;
+        }
+    }
+    for (i64 k = 2 * e; k < n; ++k) h = h + a[k] * b[k];
+    return h;
+}
+
+// out[p] = dot_product(V(:,pairs[p].x+1), V(:,pairs[p].y+1)), one lane per pair.
+__global__ __launch_bounds__(64) void k_seqdot_pairs(const double *__restrict__ V, i64 ld, i64 n,
+                                                     const short2 *__restrict__ pairs, int npairs,
+                                                     double *__restrict__ out) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= npairs) return;
+    const short2 ab = pairs[p];
+    out[p] = seq_dot(V + (i64)ab.x * ld, V + (i64)ab.y * ld, n);
+}
+
+// calculate_verr's rebuild V(:,i) = P_1..P_i e_i, level s of the reflection
+// order (:581-585: for chain i, j = i, i-1, .., 1): chain i >= s applies
+// reflector j = i - s.  k_hh_rebuild_dot: d[i] = dot_product(V(:,i), P(:,j));
+// k_hh_rebuild_upd: V(:,i) = V(:,i) - 2.0*P(:,j)*d[i] (blockIdx.y = j).
+__global__ __launch_bounds__(64) void k_hh_rebuild_dot(const double *__restrict__ Vb, const double *__restrict__ P,
+                                                       i64 ld, i64 n, int s, int n_out, double *__restrict__ d) {
+    const int i = s + blockIdx.x * 64 + threadIdx.x;
+    if (i >= n_out) return;
+    d[i] = seq_dot(Vb + (i64)i * ld, P + (i64)(i - s) * ld, n);
+}
+
+__global__ __launch_bounds__(TPB) void k_hh_rebuild_upd(double *__restrict__ Vb, const double *__restrict__ P,
+                                                        i64 ld, i64 n, int s, const double *__restrict__ d) {
+    const int j = blockIdx.y, i = s + j;
+    double *__restrict__ v = Vb + (i64)i * ld;
+    const double *__restrict__ p = P + (i64)j * ld;
+    const double dd = d[i];
+    const i64 stride = (i64)gridDim.x * TPB;
+    for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n; e += stride) v[e] = v[e] - 2.0 * p[e] * dd;
+}
+
 }  // namespace gk
 
 namespace gk {
@@ -1494,6 +1559,14 @@ constexpr int WB = GK_RES_WB;        // double2 per column per batch in flight p
 // slower (42.4 -> 46.9 us per projection at RW 80), so the default is 0.
 constexpr int XPF_MODE = GK_RES_XPF;
 constexpr bool XPF = XPF_MODE != 0;
+// TOUCH: while wave 0 runs a pass's all-gather, waves 1..3 pull the first
+// TOUCH chunks (4 KiB each) of the NEXT pass's dot column -- the one that
+// comes from HBM -- into L2 with one dword load per 128-B line into a sink
+// register, so the memory pipe works through the wait.  0 = off.
+#ifndef GK_RES_TOUCH
+#define GK_RES_TOUCH 0
+#endif
+constexpr int TOUCH = GK_RES_TOUCH;
 
 template <int RW, int LW, int MODE>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
@@ -1514,6 +1587,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
     ResClock clk;
     clk.start(a.stamps);
+    int touch_sink = 0;
     double2 wr[RW];
 #pragma unroll
     for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < nch) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
@@ -1636,13 +1710,28 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     };
     // all-gather of the partials: the same h in every workgroup (and rank)
     int xi = 0;
-    auto reduce = [&](double acc, double &h) -> bool {
+    auto reduce = [&](double acc, double &h, int touch_col) -> bool {
         clk.passed(a.stamps);
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
-        if (t < 64) res_exchange<WT / 64>(a, xi, sm, bc, &okf);
+        if (t < 64) {
+            res_exchange<WT / 64>(a, xi, sm, bc, &okf);
+        } else if constexpr (TOUCH > 0) {
+            if (touch_col >= 0) {
+                // lines [0, 32*TOUCH) of the workgroup's register-resident part of
+                // the column (contiguous from chunk c0); all loads land in one sink
+                // register, drained below before anything can reuse it
+                const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + c0 * WT);
+                const i64 lines = (i64)32 * (nch - c0 < TOUCH ? (nch - c0 > 0 ? nch - c0 : 0) : TOUCH);
+                for (i64 l = t - 64; l < lines; l += WT - 64) {
+                    const char *ptr = base + l * 128;
+                    asm volatile("global_load_dword %0, %1, off" : "+v"(touch_sink) : "v"(ptr) : "memory");
+                }
+            }
+        }
         __syncthreads();
+        if constexpr (TOUCH > 0) asm volatile("s_waitcnt vmcnt(0)" : : "v"(touch_sink) : "memory");
         ++xi;
         h = bc[0];
         clk.waited(a.stamps);
@@ -1662,7 +1751,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         if (XPF) load_first(q, q, true);
         const double acc = pass(0.0, q, q, RK_DOT);
         if (XPF) load_first(q, res_col(mode, j, 1), kind_of(0) == RK_DOT);
-        ok = reduce(acc, h);
+        ok = reduce(acc, h, kind_of(0) == RK_DOT ? res_col(mode, j, 1) : -1);
     } else {
         if (XPF) load_first(res_col(mode, j, 0), res_col(mode, j, 1), kind_of(0) == RK_DOT);
         double s = 0.0;
@@ -1681,7 +1770,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         if (mode == RES_MGS && blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
         const double acc = pass(mode == RES_MGS ? h : a.coef * h, i, res_col(mode, j, p + 1), kind);
         if (XPF && p + 1 < np) load_first(res_col(mode, j, p + 1), res_col(mode, j, p + 2), kind_of(p + 1) == RK_DOT);
-        if (kind != RK_NONE) ok = reduce(acc, h);
+        if (kind != RK_NONE) ok = reduce(acc, h, p + 1 < np && kind_of(p + 1) == RK_DOT ? res_col(mode, j, p + 2) : -1);
     }
     if (!ok) return;  // uniform per workgroup; *err is set
     if (mode != RES_MGS) {  // reflections: the resident part of w back to HBM
@@ -1705,7 +1794,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 const double x = a.w[a.n - 1];
                 acc = acc + x * x;
             }
-            ok = reduce(acc, h);
+            ok = reduce(acc, h, -1);
             if (!ok) return;
             if (blockIdx.x == 0 && t == 0) a.hs[0] = h;  // ||w(j+1:n)||^2
         }

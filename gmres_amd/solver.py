@@ -200,6 +200,13 @@ class Context:
         nat.check(nat.hip().gk_get_x(self._h, _p(x)), "gk_get_x")
         return x
 
+    def get_basis(self, col: int, which: int = 0) -> np.ndarray:
+        """Column col (0-based) of the device basis: which 0 = V (Krylov basis
+        or Householder reflectors), 1 = the basis gk_hh_verr rebuilt."""
+        v = np.empty(self.nloc, dtype=np.float64)
+        nat.check(nat.hip().gk_get_basis(self._h, which, col, _p(v)), "gk_get_basis")
+        return v
+
     def set_x(self, x: np.ndarray) -> None:
         xx = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
         nat.check(nat.hip().gk_set_x(self._h, _p(xx)), "gk_set_x")

@@ -126,6 +126,13 @@ int gk_rhs_norm(gk_ctx *ctx, double *beta0);
 /* x = 0 (x0 is always 0 in the reference, gmres_mgsr.f90:304). */
 int gk_zero_x(gk_ctx *ctx);
 int gk_get_x(gk_ctx *ctx, double *x_local);
+/* Copy column col (0-based) of a device basis to the host (nloc doubles):
+ * which = 0: V(:,col+1) -- the MGS-R Krylov basis, or the Householder
+ * reflectors P(:,col+1) (gmres_hh.f90 keeps P in the same array);
+ * which = 1: the Householder basis rebuilt by gk_hh_verr (calculate_verr's V).
+ * Diagnostic only (the orthogonality tests evaluate the reference's formula on
+ * the device basis). */
+int gk_get_basis(gk_ctx *ctx, int which, int col, double *out);
 int gk_set_x(gk_ctx *ctx, const double *x_local);
 /* Host-array operator application on this context's slab (clobbers the
  * work vectors; not between cycle start and update):  what = 0: out = A in
@@ -252,7 +259,11 @@ int gk_sync(gk_ctx *ctx);
  *                          instead of 32); 0: stream it
  *   GK_TUNE_RES_WONLY      large slabs: -1 (default) pick by the modelled bytes per projection,
  *                          1 always, 0 never the w-only variant (one wave per SIMD, ~490 registers
- *                          per lane: w in registers + LDS, both columns streamed) */
+ *                          per lane: w in registers + LDS, both columns streamed)
+ *   GK_TUNE_VERR_ORDER     1 (default): the v_err diagnostics (gk_mgs_verr, gk_hh_verr) use the
+ *                          reference's dot_product order, one running sum per dot (bit-identical
+ *                          to the reference's formula on the same basis; single rank); 0: tree
+ *                          reduction (fast; N ranks always use it) */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
@@ -267,6 +278,7 @@ int gk_sync(gk_ctx *ctx);
 #define GK_TUNE_RES_TIMEOUT_MS 11
 #define GK_TUNE_RES_LDS 12
 #define GK_TUNE_RES_WONLY 13
+#define GK_TUNE_VERR_ORDER 14
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

@@ -122,12 +122,113 @@ def test_1024_hh_three_cycles_vs_reference():
     _hist_close(r.hist_res, g["cycle_true_residual"], rtol=1e-9, atol=0.0)
 
 
-def test_mgsr_verr_small(oracle):
-    r = _solve(64, 20, "identity", max_cycles=2)
-    ref = oracle.gmres_mgsr(oracle.rhs_ones(64), 64, 20, variant=oracle.MGSR_OMP, max_cycles=2)
-    # cumulative orthogonality loss: same order of magnitude as the reference
-    a, b = r.v_err[1:r.n_out + 1], ref.v_err[1:ref.n_out + 1]
-    assert np.all(a < 1e-12) and np.all(b < 1e-12)
+# v_err by value (a9, a12, f1).  Both diagnostics measure rounding noise, and
+# the reference's own figure is dominated by the rounding of the sequential
+# dot_product that MEASURES it (one n-term running sum per dot), not by the
+# basis: a tree-reduced Gram of the same basis gives ~10x (MGS-R) / ~1000x
+# (HH) smaller values (measured on this device).  So the device evaluates the
+# diagnostics in the reference's order (GK_TUNE_VERR_ORDER, default), and
+# parity is pinned in two parts:
+#  (a) BIT-EXACT: the device-reported v_err equals the reference's formula,
+#      with the reference's dot_product (oracle.dot, 1 thread), evaluated on
+#      the host on the basis copied off the device (Householder: rebuilt from
+#      the device reflectors, and the device's rebuilt basis equals that);
+#  (b) STATISTICAL: that value against the oracle's v_err of its own run,
+#      within the oracle's own 1-vs-N-thread spread (the bases differ by
+#      reduction order only).  Spread of the oracle against itself at 1 vs
+#      2/4/8 OpenMP threads (64^2 m=20 2 cycles, 128^2 m=30 3 cycles and to
+#      convergence):
+#        MGS-R v_err(2:n_out+1): last (cumulative) entry within 0.24 decades,
+#              entrywise median <= 0.27, entrywise max 0.54 decades;
+#        HH calculate_verr(2:n_out): sum within 0.36 decades, entrywise median
+#              <= 0.65, entrywise max 2.8 decades (single terms are pure noise).
+#      Tolerances: about twice the measured spread, in decades.
+def _decades(a, b):
+    return np.abs(np.log10(np.asarray(a, dtype=np.float64) / np.asarray(b, dtype=np.float64)))
+
+
+def _mgs_verr_close(a, b):
+    d = _decades(a, b)
+    assert d[-1] <= 0.5, (a[-1], b[-1])
+    assert np.median(d) <= 0.5 and d.max() <= 1.0, d
+
+
+def _hh_verr_close(a, b, below=0.7, above=0.7):
+    """Sum within [-below, +above] decades of the oracle's; entrywise, the
+    median |decades| within 0.8 (two-sided band) or the median signed ratio
+    within [-below, +0.8] (one-sided band, below > 0.7)."""
+    a, b = np.asarray(a), np.asarray(b)
+    assert np.all(a > 0) and np.all(a < 1e-27)
+    r = np.log10(a.sum() / b.sum())
+    assert -below <= r <= above, (a.sum(), b.sum())
+    if below <= 0.7:
+        assert np.median(_decades(a, b)) <= 0.8, _decades(a, b)
+    else:
+        assert -below <= np.median(np.log10(a / b)) <= 0.8, np.log10(a / b)
+
+
+def _solve_keep(N, m, prec, method, cycles):
+    """Solve, then copy the device bases out before the context closes."""
+    import gmres_amd as ga
+
+    with ga.Context(N, m) as ctx:
+        ctx.set_precond(prec, (8.2, 0.2), 8)
+        ctx.set_rhs_ones()
+        if method == "mgsr":
+            r = ga.gmres_mgsr(ctx, 1e-15, max_cycles=cycles)
+            return r, [ctx.get_basis(k, 0) for k in range(r.n_out + 1)], None
+        r = ga.gmres_hh(ctx, 1e-15, precondition=method == "hh_prec", max_cycles=cycles)
+        return r, [ctx.get_basis(k, 0) for k in range(r.n_out)], [ctx.get_basis(k, 1) for k in range(r.n_out)]
+
+
+@pytest.mark.parametrize("N,m,cycles", [(64, 20, 2), (128, 30, 3)])
+def test_mgsr_verr_by_value(oracle, N, m, cycles):
+    """a9: the MGS-R orthogonality diagnostic (gmres_mgsr.f90:414-420)."""
+    from tests import verr_host as vh
+
+    r, V, _ = _solve_keep(N, m, "identity", "mgsr", cycles)
+    ref = oracle.gmres_mgsr(oracle.rhs_ones(N), N, m, variant=oracle.MGSR_OMP, max_cycles=cycles)
+    assert r.n_out == ref.n_out == m
+    host = vh.mgs_verr(V, m, vh.ref_dot(oracle))
+    assert np.array_equal(r.v_err[:m + 1], host[:m + 1])                   # (a)
+    _mgs_verr_close(r.v_err[1:m + 1], ref.v_err[1:m + 1])                  # (b)
+
+
+@pytest.mark.parametrize("N,m,cycles", [(64, 20, 2), (128, 30, 3)])
+@pytest.mark.parametrize("method", ["hh", "hh_prec"])
+def test_hh_verr_by_value(oracle, N, m, cycles, method):
+    """a12 / f1: calculate_verr (gmres_hh.f90:568-593) for gmres_hh_omp and
+    gmres_hh_prec_omp."""
+    from tests import verr_host as vh
+
+    prec = "identity" if method == "hh" else "cbpr2"
+    r, P, Vb = _solve_keep(N, m, prec, method, cycles)
+    ref = oracle.gmres_hh(oracle.rhs_ones(N), N, m, prec=oracle.PREC_NAMES[prec],
+                          midcycle_exit=int(method == "hh_prec"), max_cycles=cycles)
+    n = r.n_out
+    assert n == ref.n_out == m
+    dot = vh.ref_dot(oracle)
+    Vh = vh.hh_rebuild(P, n, dot)
+    assert all(np.array_equal(a, b) for a, b in zip(Vb, Vh))               # (a) the rebuilt basis
+    assert np.array_equal(r.v_err[1:n], vh.hh_verr_of_basis(Vh, n, dot)[1:n])  # (a) the diagnostic
+    _hh_verr_close(r.v_err[1:n], ref.v_err[1:n])                           # (b)
+
+
+def test_hh_verr_vs_reference_run(oracle):
+    """The reference's own 128^2 m=30 gmres_hh_omp run to convergence
+    (tests/golden/reference_runs.json; README's "~1e-30", last entry 9.5e-31).
+    After 120 cycles the device basis is MORE orthogonal than the reference's:
+    measured 1.08 decades below it (the reflectors are normalised by
+    tree-reduced norms, closer to unit length than the reference's running
+    sums make them), so the band is one-sided: never above the reference by
+    more than the thread spread, at most 1.5 decades below."""
+    from tests import verr_host as vh
+
+    ref = json.load(open(os.path.join(HERE, "golden", "reference_runs.json")))["hh_omp_identity_128_m30"]
+    r, P, _ = _solve_keep(128, 30, "identity", "hh", 1000)
+    assert r.n_out == ref["n_out"] == 30 and r.iterations == ref["iterations"]
+    assert np.array_equal(r.v_err[1:30], vh.hh_verr(P, 30, vh.ref_dot(oracle))[1:30])
+    _hh_verr_close(r.v_err[1:30], ref["v_err"][1:30], below=1.5)
 
 
 def test_true_residual_and_solution(oracle):
