@@ -822,22 +822,76 @@ int op_precond(gk_ctx *c, const double *v, double *out, bool resid, int acc, con
     return precond_sweeps(c, out, acc, vdot, part);
 }
 
+#ifndef GK_CF_JT
+#define GK_CF_JT 64  // 64: JT chosen per pass (cf_grid); any other value: that JT (A/B builds)
+#endif
+
+// Grid of a Chebyshev pass: windows of CF_PTS - 2H points across, JT grid
+// lines per workgroup.  A workgroup marches JT + 2L + 1 lines (the recompute
+// cone), so JT is chosen to minimise  rounds x (JT + 2L + 1)  where a round is
+// one wave of resident workgroups (the kernel's occupancy x CUs): at 4096^2,
+// L = 8 (252 VGPRs, 2 waves per SIMD) JT = 80 gives 1924 workgroups in ONE
+// round where 64 would need two.
+template <typename K>
+dim3 cf_grid(gk_ctx *c, K kern, int L, int &JT) {
+    const int H = L + (L & 1);
+    const int gx = (c->N + (gk::CF_PTS - 2 * H) - 1) / (gk::CF_PTS - 2 * H);
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, gk::CF_W, 0) != hipSuccess || occ <= 0) occ = 8;
+    const i64 cap = (i64)occ * std::max(1, c->res_cus > 0 ? c->res_cus : 256);
+    static const int jts[] = {16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 256, 384, 512, 1024, 2048, 4096, 8192};
+    // sized by the largest slab, so every rank writes the same number of
+    // partials (the all-reduced slab has one length on all ranks)
+    const int lines = (c->nranks > 1 && c->max_lines > c->nlines) ? c->max_lines : c->nlines;
+    i64 best = -1;
+    JT = GK_CF_JT;
+    for (int jt : jts) {
+        if (GK_CF_JT != 64 && jt != GK_CF_JT) continue;  // a fixed JT (A/B builds)
+        const i64 gy = (lines + jt - 1) / jt, nb = (i64)gx * gy;
+        if (nb > gk::NPMAX) continue;
+        const i64 cost = ((nb + cap - 1) / cap) * (jt + 2 * L + 1);
+        if (best < 0 || cost < best) {
+            best = cost;
+            JT = jt;
+        }
+        if (jt >= lines) break;
+    }
+    return dim3(gx, (lines + JT - 1) / JT, 1);
+}
+
 template <int L, bool FIRST, bool LAST>
-int launch_cf_acc(gk_ctx *c, dim3 g, int acc, const gk::CFArgs &a) {
-    if (acc == gk::ACC_DOT) gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_DOT><<<g, gk::CF_W, 0, c->st>>>(a);
-    else if (acc == gk::ACC_NORM) gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NORM><<<g, gk::CF_W, 0, c->st>>>(a);
-    else gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NONE><<<g, gk::CF_W, 0, c->st>>>(a);
+int launch_cf_acc(gk_ctx *c, int acc, gk::CFArgs &a, i64 *np) {
+    int JT;
+    dim3 g;
+    if (acc == gk::ACC_DOT) {
+        g = cf_grid(c, gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_DOT>, L, JT);
+        a.JT = JT;
+        gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_DOT><<<g, gk::CF_W, 0, c->st>>>(a);
+    } else if (acc == gk::ACC_NORM) {
+        g = cf_grid(c, gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NORM>, L, JT);
+        a.JT = JT;
+        gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NORM><<<g, gk::CF_W, 0, c->st>>>(a);
+    } else {
+        g = cf_grid(c, gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NONE>, L, JT);
+        a.JT = JT;
+        gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NONE><<<g, gk::CF_W, 0, c->st>>>(a);
+    }
     LAUNCHCHK();
+    if (np != nullptr) *np = (i64)g.x * g.y;
     return GK_OK;
 }
 
 template <bool FIRST, bool LAST>
-int launch_cf(gk_ctx *c, int L, dim3 g, int acc, const gk::CFArgs &a) {
+int launch_cf(gk_ctx *c, int L, int acc, gk::CFArgs &a, i64 *np) {
     switch (L) {
-        case 1: return launch_cf_acc<1, FIRST, LAST>(c, g, acc, a);
-        case 2: return launch_cf_acc<2, FIRST, LAST>(c, g, acc, a);
-        case 3: return launch_cf_acc<3, FIRST, LAST>(c, g, acc, a);
-        default: return launch_cf_acc<4, FIRST, LAST>(c, g, acc, a);
+        case 1: return launch_cf_acc<1, FIRST, LAST>(c, acc, a, np);
+        case 2: return launch_cf_acc<2, FIRST, LAST>(c, acc, a, np);
+        case 3: return launch_cf_acc<3, FIRST, LAST>(c, acc, a, np);
+        case 4: return launch_cf_acc<4, FIRST, LAST>(c, acc, a, np);
+        case 5: return launch_cf_acc<5, FIRST, LAST>(c, acc, a, np);
+        case 6: return launch_cf_acc<6, FIRST, LAST>(c, acc, a, np);
+        case 7: return launch_cf_acc<7, FIRST, LAST>(c, acc, a, np);
+        default: return launch_cf_acc<8, FIRST, LAST>(c, acc, a, np);
     }
 }
 
@@ -848,17 +902,6 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
     ProfScope ps(c, GK_KID_STENCIL);
     const int k = c->pdeg;
     const int g1 = std::min(k, gk::CF_LMAX), g2 = k - g1;
-    auto grid = [&](int L, int &JT) {
-        const int H = L + (L & 1);
-        const int gx = (c->N + (gk::CF_PTS - 2 * H) - 1) / (gk::CF_PTS - 2 * H);
-        JT = 64;
-        int gy = (c->nlines + JT - 1) / JT;
-        while ((i64)gx * gy > gk::NPMAX) {
-            JT *= 2;
-            gy = (c->nlines + JT - 1) / JT;
-        }
-        return dim3(gx, gy, 1);
-    };
     // On slabs every input of a pass brings L lines of each neighbour (deep halo).
     const bool slabs = collective(c) && c->nranks > 1;
     const bool has_lo = slabs && c->rank > 0, has_hi = slabs && c->rank < c->nranks - 1;
@@ -882,18 +925,17 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
         a.c1[l] = c1[l];
         a.c2[l] = c2[l];
     }
-    int JT;
-    dim3 g = grid(g1, JT);
-    a.JT = JT;
+    i64 np = 0;
     if (g2 == 0) {
         a.out = out;
-        if (acc != gk::ACC_NONE) c->last_np = g.x * g.y;
-        return launch_cf<true, true>(c, g1, g, acc, a);
+        CHK((launch_cf<true, true>(c, g1, acc, a, &np)));
+        if (acc != gk::ACC_NONE) c->last_np = (int)np;
+        return GK_OK;
     }
     a.dout = c->dA;
     a.rout = c->aux;
     a.zout = c->dB;
-    CHK((launch_cf<true, false>(c, g1, g, gk::ACC_NONE, a)));
+    CHK((launch_cf<true, false>(c, g1, gk::ACC_NONE, a, nullptr)));
     gk::CFArgs b{};
     b.N = c->N;
     b.nlines = c->nlines;
@@ -910,18 +952,17 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
         b.c1[l] = c1[g1 + l];
         b.c2[l] = c2[g1 + l];
     }
-    g = grid(g2, JT);
-    b.JT = JT;
-    if (acc != gk::ACC_NONE) c->last_np = g.x * g.y;
-    return launch_cf<false, true>(c, g2, g, acc, b);
+    CHK((launch_cf<false, true>(c, g2, acc, b, &np)));
+    if (acc != gk::ACC_NONE) c->last_np = (int)np;
+    return GK_OK;
 }
 
 // Temporal-blocked Chebyshev passes: even N (two points per lane), k <= 8,
-// and on slabs every rank holding at least CF_LMAX lines (the deep halo).
+// and on slabs every rank holding at least the first pass's L lines (the deep halo).
 bool cheb_fused_ok(gk_ctx *c) {
     if (!c->tune_cheb_fused || c->N % 2 != 0 || c->pdeg > 2 * gk::CF_LMAX) return false;
     if (!collective(c) || c->nranks == 1) return true;
-    return c->N / c->nranks >= gk::CF_LMAX;  // the smallest slab of slab_partition
+    return c->N / c->nranks >= std::min(c->pdeg, gk::CF_LMAX);  // the smallest slab of slab_partition
 }
 
 // out = M^-1 z for z already in c->z (cbpr2 or Chebyshev sweeps).

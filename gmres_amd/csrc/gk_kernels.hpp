@@ -692,7 +692,7 @@ namespace gk {
 // --------------------------------------------------------------------------
 constexpr int CF_W = 64;           // lanes per window (one wave)
 constexpr int CF_PTS = CF_W * 2;   // points per window (2 per lane)
-constexpr int CF_LMAX = 4;
+constexpr int CF_LMAX = 8;   // Chebyshev(8) = ONE pass
 
 struct CFArgs {
     const double *din;   // FIRST: z (the residual r); else d entering the group
@@ -711,9 +711,23 @@ struct CFArgs {
     const double *lo[3], *hi[3];
 };
 
+// Input prefetch depth: lines t+1 .. t+D are in flight while line t runs
+// through the levels (a D-slot ring; the time loop is unrolled by D so the
+// slots rotate by name -- a register move of an in-flight load would wait for
+// it).  The dot partner of the emitted line rides in the same ring, so no load
+// issued in the current step is waited on before the step ends.
+#ifndef GK_CF_DEPTH
+#define GK_CF_DEPTH 0
+#endif
+template <bool FIRST>
+constexpr int cf_depth() {
+    return GK_CF_DEPTH > 0 ? GK_CF_DEPTH : (FIRST ? 4 : 3);
+}
+
 template <int L, bool FIRST, bool LAST, int ACC>
 __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
     constexpr int H = L + (L & 1);                  // halo, even so a lane's 2 points are kept together
+    constexpr int D = cf_depth<FIRST>();
     const int N = a.N;
     const int lane = threadIdx.x;
     const int keep = CF_PTS - 2 * H;
@@ -753,94 +767,108 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
             v[1] = t.y;
         }
     };
-    // input line t+1 is in flight while line t runs through the levels
-    auto ld_in = [&](int row, double (&d)[2], double (&r)[2], double (&z)[2]) {
-        ld2(0, a.din, row, d);
+    // the ring: input line `row` and the dot partner of the line the last
+    // level emits when that input enters (row - L)
+    double pd[D][2], pr[D][2], pz[D][2];
+    double2 pv[D];
+    auto issue = [&](int row, int s) {
+        ld2(0, a.din, row, pd[s]);
         if (!FIRST) {
-            ld2(1, a.rin, row, r);
-            ld2(2, a.zin, row, z);
+            ld2(1, a.rin, row, pr[s]);
+            ld2(2, a.zin, row, pz[s]);
+        }
+        if (LAST && ACC == ACC_DOT) {
+            pv[s] = double2{0.0, 0.0};
+            if (row - L >= j0 && row - L < j1 && kept)
+                pv[s] = *reinterpret_cast<const double2 *>(a.vdot + (i64)(row - L) * N + i0);
         }
     };
+    const int tb0 = j0 - L - 1, tend = j1 + L;
     if (j0 < a.nlines) {
-        double nd[2], nr[2] = {0.0, 0.0}, nz[2] = {0.0, 0.0};
-        ld_in(j0 - L - 1, nd, nr, nz);
-        for (int t = j0 - L - 1; t < j1 + L; ++t) {
-            // emission of "level -1": the input line t
-            double ed[2], er[2], ez[2];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                ed[k] = nd[k];
-                er[k] = nr[k];
-                ez[k] = nz[k];
-            }
-            if (t + 1 < j1 + L) ld_in(t + 1, nd, nr, nz);
-            // the dot partner of the line the last level emits this step (row t - L)
-            double2 vd = double2{0.0, 0.0};
-            if (LAST && ACC == ACC_DOT && t - L >= j0 && t - L < j1 && kept)
-                vd = *reinterpret_cast<const double2 *>(a.vdot + (i64)(t - L) * N + i0);
-            if (FIRST) {
+        for (int s = 0; s < D; ++s)
+            if (tb0 + s < tend) issue(tb0 + s, s);
+        for (int tb = tb0; tb < tend; tb += D) {
+#pragma unroll
+            for (int s = 0; s < D; ++s) {
+                const int t = tb + s;
+                if (t >= tend) break;
+                // emission of "level -1": the input line t (slot s), then slot s
+                // refills with line t + D
+                double ed[2], er[2], ez[2];
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
-                    const double raw = ed[k];
-                    ed[k] = raw / a.theta;
-                    er[k] = raw;
-                    ez[k] = ed[k];
+                    ed[k] = pd[s][k];
+                    er[k] = FIRST ? 0.0 : pr[s][k];
+                    ez[k] = FIRST ? 0.0 : pz[s][k];
                 }
-            }
-            int row = t;  // row of the current emission
+                double2 vd = double2{0.0, 0.0};
+                if (LAST && ACC == ACC_DOT) vd = pv[s];
+                if (t + D < tend) issue(t + D, s);
+                if (FIRST) {
 #pragma unroll
-            for (int l = 0; l < L; ++l) {
-                // push the emission into level l
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    dw[l][0][k] = dw[l][1][k];
-                    dw[l][1][k] = dw[l][2][k];
-                    dw[l][2][k] = ed[k];
-                    rm[l][k] = rn[l][k];
-                    zm[l][k] = zn[l][k];
-                    rn[l][k] = er[k];
-                    zn[l][k] = ez[k];
-                }
-                // compute the middle line row-1
-                const int mrow = row - 1;
-                double left = __shfl_up(dw[l][1][1], 1, 64);
-                double right = __shfl_down(dw[l][1][0], 1, 64);
-                // a row outside the GRID is zero at every level (rows in a
-                // neighbour's halo are real; the deepest ones are wrong but
-                // never reach the kept rows -- the usual L-row recompute cone)
-                const bool rowok = (has_lo || mrow >= 0) && (has_hi || mrow < a.nlines);
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const double W = (k == 0) ? left : dw[l][1][0];
-                    const double E = (k == 1) ? right : dw[l][1][1];
-                    const double s = ((W + E) + dw[l][2][k]) + dw[l][0][k];
-                    const double ad = 4.0 * dw[l][1][k] - 1.0 * s;
-                    const double res = rm[l][k] - ad;
-                    const double dn = a.c1[l] * dw[l][1][k] + a.c2[l] * res;
-                    const double z = zm[l][k] + dn;
-                    const bool ok = rowok && (k == 0 ? in0 : in1);
-                    ed[k] = ok ? dn : 0.0;
-                    er[k] = ok ? res : 0.0;
-                    ez[k] = ok ? z : 0.0;
-                }
-                row = mrow;
-            }
-            // the last level emitted line `row`
-            if (row >= j0 && row < j1 && kept) {
-                const i64 idx = (i64)row * N + i0;
-                if (LAST) {
-                    *reinterpret_cast<double2 *>(a.out + idx) = double2{ez[0], ez[1]};
-                    if (ACC == ACC_DOT) {
-                        acc = acc + ez[0] * vd.x;
-                        acc = acc + ez[1] * vd.y;
-                    } else if (ACC == ACC_NORM) {
-                        acc = acc + ez[0] * ez[0];
-                        acc = acc + ez[1] * ez[1];
+                    for (int k = 0; k < 2; ++k) {
+                        const double raw = ed[k];
+                        ed[k] = raw / a.theta;
+                        er[k] = raw;
+                        ez[k] = ed[k];
                     }
-                } else {
-                    *reinterpret_cast<double2 *>(a.dout + idx) = double2{ed[0], ed[1]};
-                    *reinterpret_cast<double2 *>(a.rout + idx) = double2{er[0], er[1]};
-                    *reinterpret_cast<double2 *>(a.zout + idx) = double2{ez[0], ez[1]};
+                }
+                int row = t;  // row of the current emission
+#pragma unroll
+                for (int l = 0; l < L; ++l) {
+                    // push the emission into level l
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        dw[l][0][k] = dw[l][1][k];
+                        dw[l][1][k] = dw[l][2][k];
+                        dw[l][2][k] = ed[k];
+                        rm[l][k] = rn[l][k];
+                        zm[l][k] = zn[l][k];
+                        rn[l][k] = er[k];
+                        zn[l][k] = ez[k];
+                    }
+                    // compute the middle line row-1
+                    const int mrow = row - 1;
+                    double left = __shfl_up(dw[l][1][1], 1, 64);
+                    double right = __shfl_down(dw[l][1][0], 1, 64);
+                    // a row outside the GRID is zero at every level (rows in a
+                    // neighbour's halo are real; the deepest ones are wrong but
+                    // never reach the kept rows -- the usual L-row recompute cone)
+                    const bool rowok = (has_lo || mrow >= 0) && (has_hi || mrow < a.nlines);
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const double W = (k == 0) ? left : dw[l][1][0];
+                        const double E = (k == 1) ? right : dw[l][1][1];
+                        const double s2 = ((W + E) + dw[l][2][k]) + dw[l][0][k];
+                        const double ad = 4.0 * dw[l][1][k] - 1.0 * s2;
+                        const double res = rm[l][k] - ad;
+                        const double dn = a.c1[l] * dw[l][1][k] + a.c2[l] * res;
+                        const double z = zm[l][k] + dn;
+                        const bool ok = rowok && (k == 0 ? in0 : in1);
+                        ed[k] = ok ? dn : 0.0;
+                        er[k] = ok ? res : 0.0;
+                        ez[k] = ok ? z : 0.0;
+                    }
+                    row = mrow;
+                }
+                // the last level emitted line `row`
+                if (row >= j0 && row < j1 && kept) {
+                    const i64 idx = (i64)row * N + i0;
+                    if (LAST) {
+                        *reinterpret_cast<double2 *>(a.out + idx) = double2{ez[0], ez[1]};
+                        if (ACC == ACC_DOT) {
+                            acc = acc + ez[0] * vd.x;
+                            acc = acc + ez[1] * vd.y;
+                        } else if (ACC == ACC_NORM) {
+                            acc = acc + ez[0] * ez[0];
+                            acc = acc + ez[1] * ez[1];
+                        }
+                    } else {
+                        *reinterpret_cast<double2 *>(a.dout + idx) = double2{ed[0], ed[1]};
+                        *reinterpret_cast<double2 *>(a.rout + idx) = double2{er[0], er[1]};
+                        *reinterpret_cast<double2 *>(a.zout + idx) = double2{ez[0], ez[1]};
+                    }
                 }
             }
         }
@@ -1562,9 +1590,12 @@ constexpr bool XPF = XPF_MODE != 0;
 // TOUCH: while wave 0 runs a pass's all-gather, waves 1..3 pull the first
 // TOUCH chunks (4 KiB each) of the NEXT pass's dot column -- the one that
 // comes from HBM -- into L2 with one dword load per 128-B line into a sink
-// register, so the memory pipe works through the wait.  0 = off.
+// register, so the memory pipe works through the wait.  0 = off; A/B at
+// 4096^2 (profiles/r02/ab_touch*.jsonl): 8 +-0, 16 -1.5 %, 32 -2.2 % per
+// projection (MGS-R 42.4 -> 41.7 us, HH 43.2 -> 42.2 us), 48 / 64 slower
+// (the touched lines outgrow the 128 KiB per-CU share of L2).
 #ifndef GK_RES_TOUCH
-#define GK_RES_TOUCH 0
+#define GK_RES_TOUCH 32
 #endif
 constexpr int TOUCH = GK_RES_TOUCH;
 
