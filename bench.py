@@ -71,10 +71,11 @@ def prec_bytes(n: int, prec: str, degree: int, model: str) -> float:
         return 0.0
     if prec == "cbpr2":
         return float(64 * n if model == "as_written" else 16 * n)
-    # Chebyshev(k): 48n per sweep as written; the temporal-blocked passes read
-    # (d, r, z) and write them (or z alone on the last pass): 32n per pass
-    passes = (degree + 3) // 4
-    return float(48 * degree * n if model == "as_written" else 32 * passes * n)
+    # Chebyshev(k): 48n per sweep as written; fused, k <= 8 sweeps are ONE
+    # temporal-blocked pass (read z, write the result: 16n; its dot partner is
+    # the stencil launch's); each further pass of up to 8 hands over (d, r, z): +48n
+    passes = (degree + 7) // 8
+    return float(48 * degree * n if model == "as_written" else (16 + 48 * (passes - 1)) * n)
 
 
 def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str) -> float:
