@@ -317,6 +317,47 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int) -> dict
     return roof
 
 
+def diagnostics(ctx, args, run, dist, world: int) -> dict:
+    """After the timed region (not part of `value`): one more cycle with the
+    in-kernel clock split on -- per projection / reflection, the time a
+    resident launch spends streaming its pass vs waiting in the in-launch
+    all-gather (on N ranks that wait includes the cross-device rank totals) --
+    and on N ranks the collective's own latency (gk_comm_latency).  Max over
+    ranks, so the 8-GPU line carries the cross-device price beside it."""
+    import torch
+
+    m = args.m
+    if args.method == "mgsr":
+        kinds = [(0, "mgs_step", m * (m + 1))]
+    else:
+        kinds = [(1, "hh_up", m * (m + 1) // 2), (2, "hh_down", m * (m + 1) // 2 + m)]
+    ctx.res_split(1)
+    run(1)
+    ctx.sync()
+    vals = []
+    for which, _, nproj in kinds:
+        r = ctx.res_split(-1, which)
+        ok = r["launches"] > 0
+        vals += [r["pass_ms"] * 1e3 / nproj if ok else -1.0, r["wait_ms"] * 1e3 / nproj if ok else -1.0]
+    ctx.res_split(0)
+    lat = [-1.0, -1.0]
+    if world > 1:
+        c = ctx.comm_latency(200)
+        lat = [c["allreduce_us"], c["halo_us"]]
+    t = torch.tensor(vals + lat, dtype=torch.float64)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    v = [round(float(x), 3) for x in t.tolist()]
+    split = {}
+    for k, (_, name, _) in enumerate(kinds):
+        if v[2 * k] >= 0:
+            split[name] = {"pass_us": v[2 * k], "wait_us": v[2 * k + 1]}
+    return {"resident_split_per_unit_us": split or None,
+            "collective_latency_us": ({"allreduce": v[-2], "halo": v[-1]} if world > 1 else None),
+            "note": "one extra cycle after the timed region, max over ranks; pass = streaming, wait = in-launch "
+                    "all-gather (tools/res_split.py); collective = one partial-slab all-reduce / one halo exchange"}
+
+
 # ------------------------------------------------------------------- main ---
 def main() -> None:
     ap = argparse.ArgumentParser()
@@ -339,6 +380,7 @@ def main() -> None:
     ap.add_argument("--prof-every", type=int, default=16,
                     help="HIP events around the launches of every S-th Arnoldi step (1 = all)")
     ap.add_argument("--plan-only", action="store_true", help="print the multi-GPU launch plan and exit")
+    ap.add_argument("--no-diag", action="store_true", help="skip the post-timing diagnostic cycle")
     args = ap.parse_args()
     maybe_self_launch(args, sys.argv[1:])
 
@@ -436,6 +478,7 @@ def main() -> None:
         elapsed = float(t.item())
     cycles = res.n_cycles
     iters = (cycles - 1) * m + res.n_out if cycles > 0 else 0
+    diag = None if args.no_diag else diagnostics(ctx, args, run, dist, world)
 
     if rank == 0:
         n = N * N
@@ -474,6 +517,7 @@ def main() -> None:
             "alg_as_written_frac": round(b_written / elapsed / 1e9 / HBM_PEAK_GBPS, 4) if full else None,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "diagnostics": diag,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -57,6 +57,7 @@ _SIGS = {
     "gk_comm_init": (c_int, [c_vp, c_int, c_int, c_int, ctypes.c_char_p]),
     "gk_local_size": (c_int, [c_vp, ctypes.POINTER(c_ll)]),
     "gk_comm_info": (c_int, [c_vp, _ip, _ip]),
+    "gk_comm_latency": (c_int, [c_vp, c_int, _dp, _dp]),
     "gk_group_create": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "gk_group_destroy": (c_int, [c_vp]),
     "gk_comm_init_local": (c_int, [c_vp, c_vp, c_int, c_int]),

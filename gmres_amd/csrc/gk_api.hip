@@ -1462,6 +1462,35 @@ int gk_xchg_selftest(gk_ctx *c, int timeout_ms) {
     return GK_OK;
 }
 
+int gk_comm_latency(gk_ctx *c, int iters, double *allreduce_us, double *halo_us) {
+    CHK(check_ctx(c));
+    if (iters < 1 || allreduce_us == nullptr || halo_us == nullptr) return set_err(GK_ERR_ARG, "bad arguments");
+    *allreduce_us = *halo_us = 0.0;
+    if (!collective(c)) return GK_OK;
+    HIPCHK(hipSetDevice(c->dev));
+    hipEvent_t e[3];
+    for (auto &x : e) HIPCHK(hipEventCreate(&x));
+    double *buf = slot(c, 0);
+    const int count = std::max(1, c->np_pj);  // one projection's partial slab, as the launch path sends it
+    int rc = allreduce(c, buf, count);         // warm: first-call setup stays out of the timing
+    if (rc == GK_OK) rc = halo(c, c->w);
+    if (rc == GK_OK) rc = hipEventRecord(e[0], c->st) == hipSuccess ? GK_OK : GK_ERR_HIP;
+    for (int i = 0; i < iters && rc == GK_OK; ++i) rc = allreduce(c, buf, count);
+    if (rc == GK_OK) rc = hipEventRecord(e[1], c->st) == hipSuccess ? GK_OK : GK_ERR_HIP;
+    for (int i = 0; i < iters && rc == GK_OK; ++i) rc = halo(c, c->w);
+    if (rc == GK_OK) rc = hipEventRecord(e[2], c->st) == hipSuccess ? GK_OK : GK_ERR_HIP;
+    if (rc == GK_OK) rc = sync_st(c);
+    float a = 0.f, b = 0.f;
+    if (rc == GK_OK && (hipEventElapsedTime(&a, e[0], e[1]) != hipSuccess ||
+                        hipEventElapsedTime(&b, e[1], e[2]) != hipSuccess))
+        rc = set_err(GK_ERR_HIP, "event timing failed");
+    for (auto &x : e) (void)hipEventDestroy(x);
+    if (rc != GK_OK) return rc;
+    *allreduce_us = 1e3 * a / iters;
+    *halo_us = 1e3 * b / iters;
+    return GK_OK;
+}
+
 int gk_comm_info(gk_ctx *c, int *kind, int *nranks_seen) {
     if (c == nullptr || kind == nullptr || nranks_seen == nullptr) return set_err(GK_ERR_ARG, "null argument");
     *kind = GK_COMM_NONE;

@@ -165,6 +165,13 @@ class Context:
         nat.check(nat.hip().gk_comm_info(self._h, ctypes.byref(k), ctypes.byref(nr)), "gk_comm_info")
         return {"kind": nat.COMM_KINDS.get(k.value, k.value), "nranks": nr.value}
 
+    def comm_latency(self, iters: int = 200) -> dict:
+        """Collective (all ranks): mean us of one partial-slab all-reduce and
+        one halo exchange through the collective in use (gk_comm_latency)."""
+        a, h = ctypes.c_double(), ctypes.c_double()
+        nat.check(nat.hip().gk_comm_latency(self._h, iters, ctypes.byref(a), ctypes.byref(h)), "gk_comm_latency")
+        return {"allreduce_us": a.value, "halo_us": h.value}
+
     def xchg_selftest(self, timeout_ms: int = 5000) -> bool:
         """Collective self-test of the device exchange; False (and the
         exchange disabled on this rank) when it fails."""

@@ -113,6 +113,13 @@ int gk_local_size(gk_ctx *ctx, long long *nloc);
 #define GK_COMM_LOCAL 2
 #define GK_COMM_XGMI 3
 int gk_comm_info(gk_ctx *ctx, int *kind, int *nranks_seen);
+/* Collective, every rank together: the mean cost (us, HIP events on the
+ * context stream) of one all-reduce of a projection's partial slab and of one
+ * halo exchange (one grid line with each neighbour) through the collective in
+ * use (device exchange, RCCL or the local group), over `iters` back-to-back
+ * calls.  Diagnostic (bench.py reports it beside a multi-GPU line); leaves
+ * the reduction slots and halo buffers overwritten. */
+int gk_comm_latency(gk_ctx *ctx, int iters, double *allreduce_us, double *halo_us);
 
 /* Preconditioner: kind GK_PREC_*, params (cbpr2: params[0..1] as
  * chebyshev.f90:19-25; CHEB: interval ends params[0..1]), degree (CHEB only). */

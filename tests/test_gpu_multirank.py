@@ -179,3 +179,31 @@ def test_chebyshev_on_slabs_bitexact(oracle, N, nranks, degree):
         for c in ctxs:
             c.close()
         g.close()
+
+
+def test_comm_latency_local_group_and_single():
+    """gk_comm_latency through the in-process group (RCCL's message pattern),
+    and zeros on a single context (no collective)."""
+    import threading
+
+    import gmres_amd as ga
+
+    with ga.Context(32, 4) as c:
+        assert c.comm_latency(10) == {"allreduce_us": 0.0, "halo_us": 0.0}
+    parts = ga.slab_partition(64, 2)
+    g = ga.LocalGroup(2)
+    ctxs = [ga.Context(64, 8, device=0, line0=l0, nlines=nl) for l0, nl in parts]
+    out = [None, None]
+    try:
+        for r, c in enumerate(ctxs):
+            c.comm_init_local(g, r, max(nl for _, nl in parts))
+        th = [threading.Thread(target=lambda r=r: out.__setitem__(r, ctxs[r].comm_latency(20))) for r in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert all(o is not None and o["allreduce_us"] > 0 and o["halo_us"] > 0 for o in out), out
+    finally:
+        for c in ctxs:
+            c.close()
+        g.close()

@@ -262,3 +262,19 @@ def test_chebyshev_deep_halo_over_device_exchange(oracle, N, nranks, degree):
     out = _run_threads(nranks, lambda q: ctxs[q].apply(r[parts[q][0] * N:(parts[q][0] + parts[q][1]) * N], 1))
     _close(g, ctxs)
     assert np.array_equal(np.concatenate(out), ref)
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_comm_latency_diagnostic(nranks):
+    """gk_comm_latency (bench.py's multi-GPU diagnostic) through the device
+    exchange: every rank returns a positive per-op cost, and the exchange still
+    gives bit-identical slab solves afterwards."""
+    g, ctxs = _local_group(64, 8, nranks)
+    try:
+        lat = _run_threads(nranks, lambda r: ctxs[r].comm_latency(50))
+        for d in lat:
+            assert 0.0 < d["allreduce_us"] < 5e4 and 0.0 < d["halo_us"] < 5e4, lat
+        res = _run_threads(nranks, lambda r: (ctxs[r].set_rhs_ones(), _solve(ctxs[r], "mgsr", "identity", 2))[1])
+        assert all(np.array_equal(res[0].hist_res, r.hist_res) for r in res)
+    finally:
+        _close(g, ctxs)
