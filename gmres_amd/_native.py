@@ -93,6 +93,7 @@ _SIGS = {
     "gk_profile_reset": (c_int, [c_vp]),
     "gk_profile_read": (c_int, [c_vp, c_int, _dp, ctypes.POINTER(c_ll)]),
     "gk_sync": (c_int, [c_vp]),
+    "gk_profile_res_wg": (c_int, [c_vp, c_int, _dp, _dp, c_int, _ip]),
     "gk_profile_res_split": (c_int, [c_vp, c_int, c_int, _dp, _dp, _dp, ctypes.POINTER(c_ll)]),
     "gk_set_tuning": (c_int, [c_vp, c_int, c_int]),
     "gk_lanczos_bounds": (c_int, [c_vp, c_int, _dp, _dp]),

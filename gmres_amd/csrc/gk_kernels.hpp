@@ -1101,6 +1101,8 @@ struct ResArgs {
     unsigned tag0;        // granule tag of exchange p = tag0 + p (never 0)
     int j;
     i64 n, nres2;         // local length; resident double2 prefix
+    int r2e, l2e;         // chunks per workgroup actually resident in registers / LDS (<= the
+                          // template's R2 / L2): the resident prefix is spread evenly
     XsPeers peers;        // nranks > 1: device exchange regions
     int nranks, rank;
     unsigned xseq0;       // exchange p uses sequence number xseq0 + 1 + p
@@ -1313,8 +1315,8 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
     // DT), so the test is uniform and every address is a uniform base + td*16.
     // [nres2, n2) streams through w in HBM as in k_proj.
     const i64 nch = a.nres2 / DT;
-    const i64 c0 = (i64)blockIdx.x * R2;
-    const i64 l0 = (i64)gridDim.x * R2 + (i64)blockIdx.x * L2;
+    const i64 c0 = (i64)blockIdx.x * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
+    const i64 l0 = (i64)gridDim.x * a.r2e + (i64)blockIdx.x * a.l2e, lend = l0 + a.l2e < nch ? l0 + a.l2e : nch;
     const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
     double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
     auto colchunk = [&](int col, i64 c) { return V2 + (i64)col * ld2 + c * DT; };
@@ -1323,7 +1325,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
     for (int k = 0; k < R2; ++k) {  // zeros past nres2: they add exact zeros to every dot
         wr[k] = xa[k] = double2{0.0, 0.0};
         if constexpr (PF) xb[k] = double2{0.0, 0.0};
-        if (data && c0 + k < nch) {
+        if (data && c0 + k < cend) {
             wr[k] = W2[(c0 + k) * DT + td];
             xa[k] = colchunk(res_col(mode, j, 0), c0 + k)[td];              // AXPY partner of projection 0
             if constexpr (PF) xb[k] = colchunk(res_col(mode, j, 1), c0 + k)[td];  // its dot partner
@@ -1331,7 +1333,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
     }
     if constexpr (L2 > 0) {
         for (int k = 0; k < L2; ++k)
-            if (data && l0 + k < nch) lw[k * DT + td] = W2[(l0 + k) * DT + td];
+            if (data && l0 + k < lend) lw[k * DT + td] = W2[(l0 + k) * DT + td];
     }
     const i64 sstride = (i64)gridDim.x * DT;
     const i64 sbase = a.nres2 + (i64)blockIdx.x * DT + td;
@@ -1352,7 +1354,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
             }
             if constexpr (L2 > 0) {
                 for (int k = 0; k < L2; ++k)
-                    if (l0 + k < nch) {
+                    if (l0 + k < lend) {
                         const double2 wv = lw[k * DT + td], bv = ldv<NT>(B2 + (l0 + k) * DT + td);
                         acc = acc + wv.x * bv.x;
                         acc = acc + wv.y * bv.y;
@@ -1410,7 +1412,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
             } else {
 #pragma unroll
                 for (int k = 0; k < R2; ++k)
-                    if (c0 + k < nch) X[k] = ldv<NT>(colchunk(q, c0 + k) + td);
+                    if (c0 + k < cend) X[k] = ldv<NT>(colchunk(q, c0 + k) + td);
 #pragma unroll
                 for (int k = 0; k < R2; ++k) {
                     acc = acc + wr[k].x * X[k].x;
@@ -1425,7 +1427,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
                         const i64 c = l0 + k + u;
-                        if (k + u < L2 && c < nch) {
+                        if (k + u < L2 && c < lend) {
                             wv[u] = lw[(k + u) * DT + td];
                             av[u] = ldv<NT>(A2 + c * DT + td);
                             if (!last) bv[u] = ldv<NT>(B2 + c * DT + td);
@@ -1434,7 +1436,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
                         const i64 c = l0 + k + u;
-                        if (k + u < L2 && c < nch) {
+                        if (k + u < L2 && c < lend) {
                             wv[u].x = wv[u].x - ch * av[u].x;
                             wv[u].y = wv[u].y - ch * av[u].y;
                             lw[(k + u) * DT + td] = wv[u];
@@ -1495,7 +1497,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                 const int q2 = res_col(mode, j, p + 2);
 #pragma unroll
                 for (int k = 0; k < R2; ++k)
-                    if (c0 + k < nch) X[k] = ldv<NT>(colchunk(q2, c0 + k) + td);
+                    if (c0 + k < cend) X[k] = ldv<NT>(colchunk(q2, c0 + k) + td);
             }
         }
         if (t < 64) res_exchange(a, xi, sm, bc, &okf);
@@ -1518,10 +1520,10 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         if (data) {
 #pragma unroll
             for (int k = 0; k < R2; ++k)
-                if (c0 + k < nch) W2[(c0 + k) * DT + td] = wr[k];
+                if (c0 + k < cend) W2[(c0 + k) * DT + td] = wr[k];
             if constexpr (L2 > 0) {
                 for (int k = 0; k < L2; ++k)
-                    if (l0 + k < nch) W2[(l0 + k) * DT + td] = lw[k * DT + td];
+                    if (l0 + k < lend) W2[(l0 + k) * DT + td] = lw[k * DT + td];
             }
         }
         if (mode == RES_HH_UP && blockIdx.x == 0 && t == 0) a.hs[0] = h;  // ||w(j+1:n)||^2
@@ -1534,11 +1536,11 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
     if (data) {
 #pragma unroll
         for (int k = 0; k < R2; ++k)
-            if (c0 + k < nch)
+            if (c0 + k < cend)
                 O2[(c0 + k) * DT + td] = hn != 0.0 ? double2{wr[k].x / hn, wr[k].y / hn} : double2{0.0, 0.0};
         if constexpr (L2 > 0) {
             for (int k = 0; k < L2; ++k)
-                if (l0 + k < nch) {
+                if (l0 + k < lend) {
                     const double2 v = lw[k * DT + td];
                     O2[(l0 + k) * DT + td] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
                 }
@@ -1611,8 +1613,8 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     const int j = a.j, np = res_np(mode, j);
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
     const i64 nch = a.nres2 / WT;
-    const i64 c0 = (i64)blockIdx.x * RW;
-    const i64 l0 = (i64)gridDim.x * RW + (i64)blockIdx.x * LW;
+    const i64 c0 = (i64)blockIdx.x * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
+    const i64 l0 = (i64)gridDim.x * a.r2e + (i64)blockIdx.x * a.l2e, lend = l0 + a.l2e < nch ? l0 + a.l2e : nch;
     const i64 tail0 = mode == RES_HH_UP ? a.tail0 : 0;
     const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
     double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
@@ -1621,9 +1623,9 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     int touch_sink = 0;
     double2 wr[RW];
 #pragma unroll
-    for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < nch) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
+    for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
     for (int k = 0; k < LW; ++k)
-        if (l0 + k < nch) lw[k * WT + t] = W2[(l0 + k) * WT + t];
+        if (l0 + k < lend) lw[k * WT + t] = W2[(l0 + k) * WT + t];
     const i64 sstride = (i64)gridDim.x * WT;
     const i64 sbase = a.nres2 + (i64)blockIdx.x * WT + t;
     // acc += the closing reduction of element pair e2 (local double2 index)
@@ -1647,7 +1649,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 #pragma unroll
         for (int u = 0; u < WB; ++u) {
             const i64 c = c0 + u;
-            if (u < RW && c < nch) {
+            if (u < RW && c < cend) {
                 pa[u] = ldv<true>(A2 + c * WT + t);
                 if (dot) pb[u] = B2[c * WT + t];
             }
@@ -1670,7 +1672,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 if (XPF && k0 == 0 && xpf_wave) {
                     av[u] = pa[u];
                     bv[u] = pb[u];
-                } else if (k0 + u < RW && c < nch) {
+                } else if (k0 + u < RW && c < cend) {
                     av[u] = ldv<true>(A2 + c * WT + t);
                     if (dot) bv[u] = B2[c * WT + t];
                 }
@@ -1678,7 +1680,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
                 const int k = k0 + u;
-                if (k < RW && c0 + k < nch) {
+                if (k < RW && c0 + k < cend) {
                     wr[k].x = wr[k].x - ch * av[u].x;
                     wr[k].y = wr[k].y - ch * av[u].y;
                     red(acc, wr[k], bv[u], kind, (c0 + k) * WT + t, mode == RES_HH_UP && c0 + k == 0);
@@ -1691,7 +1693,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
                 const i64 c = l0 + k0 + u;
-                if (k0 + u < LW && c < nch) {
+                if (k0 + u < LW && c < lend) {
                     av[u] = ldv<true>(A2 + c * WT + t);
                     if (dot) bv[u] = B2[c * WT + t];
                 }
@@ -1699,7 +1701,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
                 const int k = k0 + u;
-                if (k < LW && l0 + k < nch) {
+                if (k < LW && l0 + k < lend) {
                     double2 wv = lw[k * WT + t];
                     wv.x = wv.x - ch * av[u].x;
                     wv.y = wv.y - ch * av[u].y;
@@ -1754,7 +1756,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 // the column (contiguous from chunk c0); all loads land in one sink
                 // register, drained below before anything can reuse it
                 const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + c0 * WT);
-                const i64 lines = (i64)32 * (nch - c0 < TOUCH ? (nch - c0 > 0 ? nch - c0 : 0) : TOUCH);
+                const i64 lines = (i64)32 * (cend - c0 < TOUCH ? (cend - c0 > 0 ? cend - c0 : 0) : TOUCH);
                 for (i64 l = t - 64; l < lines; l += WT - 64) {
                     const char *ptr = base + l * 128;
                     asm volatile("global_load_dword %0, %1, off" : "+v"(touch_sink) : "v"(ptr) : "memory");
@@ -1809,12 +1811,12 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         const bool up = mode == RES_HH_UP;
 #pragma unroll
         for (int k = 0; k < RW; ++k)
-            if (c0 + k < nch) {
+            if (c0 + k < cend) {
                 W2[(c0 + k) * WT + t] = wr[k];
                 if (up) sq_acc(acc, wr[k], (c0 + k) * WT + t, tail0, c0 + k == 0);
             }
         for (int k = 0; k < LW; ++k)
-            if (l0 + k < nch) {
+            if (l0 + k < lend) {
                 const double2 v = lw[k * WT + t];
                 W2[(l0 + k) * WT + t] = v;
                 if (up) sq_acc(acc, v, (l0 + k) * WT + t, tail0, l0 + k == 0);
@@ -1836,10 +1838,10 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     double2 *__restrict__ O2 = reinterpret_cast<double2 *>(a.vout);
 #pragma unroll
     for (int k = 0; k < RW; ++k)
-        if (c0 + k < nch)
+        if (c0 + k < cend)
             O2[(c0 + k) * WT + t] = hn != 0.0 ? double2{wr[k].x / hn, wr[k].y / hn} : double2{0.0, 0.0};
     for (int k = 0; k < LW; ++k)
-        if (l0 + k < nch) {
+        if (l0 + k < lend) {
             const double2 v = lw[k * WT + t];
             O2[(l0 + k) * WT + t] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
         }

@@ -283,6 +283,15 @@ class Context:
                                                  ctypes.byref(t), ctypes.byref(n)), "gk_profile_res_split")
         return {"pass_ms": p.value, "wait_ms": w.value, "total_ms": t.value, "launches": int(n.value)}
 
+    def res_split_wg(self, which: int = 0) -> tuple[np.ndarray, np.ndarray]:
+        """Per-workgroup pass / wait ms of the resident launches (gk_profile_res_wg)."""
+        p = np.zeros(1024)
+        w = np.zeros(1024)
+        n = ctypes.c_int()
+        nat.check(nat.hip().gk_profile_res_wg(self._h, int(which), _p(p), _p(w), 1024, ctypes.byref(n)),
+                  "gk_profile_res_wg")
+        return p[: n.value], w[: n.value]
+
     def tune(self, key: int, value: int) -> None:
         """Launch-policy knob (include/gmres_hip.h GK_TUNE_*)."""
         nat.check(nat.hip().gk_set_tuning(self._h, int(key), int(value)), "gk_set_tuning")

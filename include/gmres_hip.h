@@ -234,6 +234,9 @@ int gk_profile_read(gk_ctx *ctx, int kid, double *total_ms, long long *launches)
  * pointers may be NULL to skip reading). */
 int gk_profile_res_split(gk_ctx *ctx, int mode, int which, double *pass_ms, double *wait_ms, double *total_ms,
                          long long *launches);
+/* The same split per workgroup (blockIdx order, summed over launches): the
+ * arrival skew of the in-launch all-gathers shows as the spread of pass_ms. */
+int gk_profile_res_wg(gk_ctx *ctx, int which, double *pass_ms, double *wait_ms, int maxwg, int *nwg);
 int gk_sync(gk_ctx *ctx);
 
 /* Launch-policy knobs (defaults are the tuned values; for A/B measurement).

@@ -11,6 +11,8 @@ import json
 import os
 import sys
 
+import numpy as np
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -48,6 +50,12 @@ def main() -> None:
                                        "wait": round(r["wait_ms"] * 1e3 / nproj, 3),
                                        "total": round(r["total_ms"] * 1e3 / nproj, 3)},
                        "units": nproj}
+                pw, ww = c.res_split_wg(which)
+                if len(pw):  # arrival skew: per-workgroup pass time, and by XCD (blockIdx % 8)
+                    per = pw * 1e3 / nproj
+                    out["wg_pass_us"] = {"min": round(float(per.min()), 3), "median": round(float(np.median(per)), 3),
+                                         "max": round(float(per.max()), 3)}
+                    out["xcd_pass_us"] = [round(float(per[k::8].mean()), 3) for k in range(min(8, len(per)))]
                 print(json.dumps(out), flush=True)
             c.res_split(0)
 
