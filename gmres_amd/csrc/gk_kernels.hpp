@@ -1196,6 +1196,14 @@ __device__ __forceinline__ double block_sum_rt(double v, double *sm) {
 // G partials of the grid (8 granules in flight per lane) and sum them in a
 // fixed order; on N ranks then add the rank totals in rank order.  Result in
 // bc[0]; *okf = 0 when a deadline passed (then *err is set).
+#ifndef GK_RES_POLL_SLEEP
+#define GK_RES_POLL_SLEEP 16
+#endif
+// s_sleep units (64 clocks) between unanswered polls.  A/B (profiles/r02/ab_poll_*.jsonl):
+// 1 / 4 / 16 / 48 -> 4096^2 42.1 / 42.1 / 41.7 / 41.6 us, 1024^2 4.42 / 4.45 / 4.40 / 4.81 us per
+// projection: continuous polls by early finishers slow the stragglers' streams.
+constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
+
 template <int NW = RWAVES>
 __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const double *sm, double *bc, int *okf) {
     const int lane = threadIdx.x;
@@ -1220,16 +1228,22 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
     for (int c0 = 0; c0 < 2 * G && all_ok; c0 += 512) {
         unsigned v[8];
         for (;;) {
-            bool ok = true;
+            // All 8 loads unconditionally (out-of-range lanes re-read granule 0
+            // and ignore it): a per-load bounds branch made the compiler wait for
+            // each load before issuing the next -- 8 serial round trips to the
+            // point of coherence per poll instead of one.
+            u64 x[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int g = c0 + lane + 64 * k;
-                v[k] = 0;
-                if (g < 2 * G) {
-                    const u64 x = __hip_atomic_load(slot + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    v[k] = (unsigned)x;
-                    ok = ok && (unsigned)(x >> 32) == tag;
-                }
+                x[k] = __hip_atomic_load(slot + (g < 2 * G ? g : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const bool in = c0 + lane + 64 * k < 2 * G;
+                v[k] = in ? (unsigned)x[k] : 0u;
+                ok = ok && (!in || (unsigned)(x[k] >> 32) == tag);
             }
             if (__all(ok)) break;
             if (wall_clock64() > deadline) {
@@ -1246,7 +1260,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
                 if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(RES_POLL_SLEEP);
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {  // workgroups in increasing order per lane pair
