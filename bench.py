@@ -215,7 +215,7 @@ def maybe_self_launch(args, argv: list[str]) -> None:
     import torch
 
     vis = torch.cuda.device_count()  # counting devices does not initialise them on this image
-    if vis < args.gpus:
+    if vis < args.gpus and os.environ.get("GK_BENCH_SAME_DEVICE") != "1":
         print(f"bench.py: --gpus {args.gpus} but only {vis} GPU(s) visible", file=sys.stderr)
         sys.exit(2)
     env = dict(os.environ, **plan["env"])
@@ -389,6 +389,11 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N-rank flow on a 1-GPU box (tests only, never a bench
+    # line): every rank on device 0, resident launches sharing its CUs.
+    same_dev = os.environ.get("GK_BENCH_SAME_DEVICE") == "1"
+    if same_dev:
+        local = 0
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
@@ -404,6 +409,8 @@ def main() -> None:
     parts = ga.slab_partition(N, world)
     line0, nlines = parts[rank]
     ctx = ga.Context(N, m, device=local, line0=line0, nlines=nlines)
+    if same_dev and world > 1:
+        ctx.tune(10, world)  # GK_TUNE_RES_SHARE
     ml = max(p[1] for p in parts)
     collective = None
     if world > 1 and args.collective == "xgmi":

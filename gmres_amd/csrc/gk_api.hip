@@ -764,7 +764,7 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
     ProfScope ps(c, GK_KID_RES);
     const int np = mode == gk::RES_MGS ? 2 * j : j;  // exchanges of the launch
     if (c->res_tag > 0xF0000000u) {  // tags must never repeat within the granule region's lifetime
-        HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * 4 * gk::RGMAX, c->st));
+        HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_WORDS, c->st));
         c->res_tag = 1;
     }
     gk::ResArgs a{};
@@ -1190,10 +1190,10 @@ int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out)
         hipHostMalloc(&c->hallh, sizeof(double) * (size_t)(m + 2) * (m + 1), hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void **)&c->hallh_dev, c->hallh, 0) != hipSuccess)
         return fail(set_err(GK_ERR_NOMEM, "cannot allocate the Hessenberg mirrors"));
-    if (hipMalloc(&c->res_gath, sizeof(gk::u64) * 4 * gk::RGMAX) != hipSuccess ||
+    if (hipMalloc(&c->res_gath, sizeof(gk::u64) * gk::RES_GATH_WORDS) != hipSuccess ||
         hipHostMalloc((void **)&c->res_err, sizeof(int), hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void **)&c->res_err_dev, c->res_err, 0) != hipSuccess ||
-        hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * 4 * gk::RGMAX, c->st) != hipSuccess)
+        hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_WORDS, c->st) != hipSuccess)
         return fail(set_err(GK_ERR_NOMEM, "cannot allocate the resident-step exchange area"));
     *c->res_err = 0;
     {

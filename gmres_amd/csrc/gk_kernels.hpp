@@ -1196,6 +1196,19 @@ __device__ __forceinline__ double block_sum_rt(double v, double *sm) {
 // G partials of the grid (8 granules in flight per lane) and sum them in a
 // fixed order; on N ranks then add the rank totals in rank order.  Result in
 // bc[0]; *okf = 0 when a deadline passed (then *err is set).
+#ifndef GK_RES_XHOPS
+#define GK_RES_XHOPS 2
+#endif
+// 1: every workgroup sweeps all partials; 2: via group leaders, in the
+// small-grid kernel (k_mgs_res with a control wave) only.  A/B
+// (profiles/r02/ab_hops_*.jsonl): two hops 4.25 vs 4.37 us per projection at
+// 1024^2, but 10.9 vs 10.4 at 2048^2 and 43.2 vs 41.6 at 4096^2, where the
+// flat sweep is not the congested part and the second round trip costs.
+constexpr int RES_XHOPS = GK_RES_XHOPS;
+constexpr int RES_NG = 8;                     // groups of the two-hop all-gather (blockIdx % 8)
+constexpr int RES_MK = (2 * RGMAX / RES_NG + 63) / 64;  // granule loads per lane of a leader's sweep
+constexpr i64 RES_GATH_WORDS = 4 * (i64)RGMAX + 4 * RES_NG;  // [2][RGMAX][2] partials + [2][NG][2] group sums
+
 #ifndef GK_RES_POLL_SLEEP
 #define GK_RES_POLL_SLEEP 16
 #endif
@@ -1204,7 +1217,7 @@ __device__ __forceinline__ double block_sum_rt(double v, double *sm) {
 // projection: continuous polls by early finishers slow the stragglers' streams.
 constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
 
-template <int NW = RWAVES>
+template <int NW = RWAVES, bool HOP2 = false>
 __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const double *sm, double *bc, int *okf) {
     const int lane = threadIdx.x;
     const int G = gridDim.x;
@@ -1223,54 +1236,139 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
     const u64 deadline = wall_clock64() + a.timeout;
     double acc = 0.0;
     bool all_ok = true;
-    // Lane L holds granule L + 64k of each 512-granule sweep: the lo (even L)
-    // or hi (odd L) half of workgroup c0/2 + L/2 + 32k.
-    for (int c0 = 0; c0 < 2 * G && all_ok; c0 += 512) {
-        unsigned v[8];
-        for (;;) {
-            // All 8 loads unconditionally (out-of-range lanes re-read granule 0
-            // and ignore it): a per-load bounds branch made the compiler wait for
-            // each load before issuing the next -- 8 serial round trips to the
-            // point of coherence per poll instead of one.
-            u64 x[8];
+    if (HOP2 && RES_XHOPS == 2 && G > 2 * RES_NG) {
+        // Two hops.  Hop 1: the leader of group g (workgroup g < RES_NG) sweeps
+        // the granules of its members g, g + NG, g + 2NG, ... (under round-robin
+        // dispatch one XCD's workgroups: same-XCD traffic, never assumed for
+        // correctness) and publishes their sum, in member order, as a granule
+        // pair.  Hop 2: every workgroup reads the NG group sums and adds them in
+        // group order.  256 readers of 16 granules instead of 256 readers of
+        // 2G: the sweep load that queued at the granules' memory channel.
+        u64 *gs = a.gath + 4 * (i64)RGMAX + (i64)(p & 1) * RES_NG * 2;
+        if ((int)blockIdx.x < RES_NG) {
+            const int g = blockIdx.x;
+            const int nmem = (G - 1 - g) / RES_NG + 1;  // members of group g
+            unsigned v[RES_MK];
+            for (;;) {
+                u64 x[RES_MK];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int g = c0 + lane + 64 * k;
-                x[k] = __hip_atomic_load(slot + (g < 2 * G ? g : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            bool ok = true;
+                for (int k = 0; k < RES_MK; ++k) {  // granule gi = lane + 64k of the group: member gi/2, half gi&1
+                    const int gi = lane + 64 * k, b = g + RES_NG * (gi >> 1);
+                    x[k] = __hip_atomic_load(slot + (gi < 2 * nmem ? 2 * b + (gi & 1) : 0), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                }
+                bool ok = true;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const bool in = c0 + lane + 64 * k < 2 * G;
-                v[k] = in ? (unsigned)x[k] : 0u;
-                ok = ok && (!in || (unsigned)(x[k] >> 32) == tag);
+                for (int k = 0; k < RES_MK; ++k) {
+                    const bool in = lane + 64 * k < 2 * nmem;
+                    v[k] = in ? (unsigned)x[k] : 0u;
+                    ok = ok && (!in || (unsigned)(x[k] >> 32) == tag);
+                }
+                if (__all(ok)) break;
+                if (wall_clock64() > deadline) {
+                    all_ok = false;
+                    int miss = 0x7FFF;
+#pragma unroll
+                    for (int k = 0; k < RES_MK; ++k) {
+                        const int gi = lane + 64 * k;
+                        if (gi < 2 * nmem && (unsigned)(x[k] >> 32) != tag) miss = min(miss, g + RES_NG * (gi >> 1));
+                    }
+                    for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, 64));
+                    if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(RES_POLL_SLEEP);
             }
+            double gsum = 0.0;
+#pragma unroll
+            for (int k = 0; k < RES_MK; ++k) {  // members in increasing order per lane pair
+                const unsigned o = __shfl_xor(v[k], 1, 64);
+                const unsigned lo = (lane & 1) ? o : v[k], hi = (lane & 1) ? v[k] : o;
+                if (!(lane & 1) && lane + 64 * k < 2 * nmem)
+                    gsum = gsum + __longlong_as_double((long long)(((u64)hi << 32) | lo));
+            }
+            gsum = wave_sum(gsum);
+            if (lane < 2 && all_ok) {
+                const u64 bits = (u64)__double_as_longlong(gsum);
+                __hip_atomic_store(gs + 2 * g + lane, ((u64)tag << 32) | (lane ? (unsigned)(bits >> 32) : (unsigned)bits),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        // hop 2: lanes 0 .. 2NG-1 hold the halves of the group sums
+        unsigned d = 0;
+        while (all_ok) {
+            const u64 x = __hip_atomic_load(gs + (lane < 2 * RES_NG ? lane : 0), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+            const bool ok = lane >= 2 * RES_NG || (unsigned)(x >> 32) == tag;
+            d = (unsigned)x;
             if (__all(ok)) break;
             if (wall_clock64() > deadline) {
                 all_ok = false;
-                int miss = 0x7FFF;  // the lowest workgroup whose granule never came
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int g = c0 + lane + 64 * k;
-                    if (g < 2 * G && (unsigned)(__hip_atomic_load(slot + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                >> 32) != tag)
-                        miss = min(miss, g >> 1);
-                }
+                int miss = ok ? 0x7FFF : (lane >> 1);
                 for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, 64));
-                if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
+                if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);  // the leader of the missing group
                 break;
             }
             __builtin_amdgcn_s_sleep(RES_POLL_SLEEP);
         }
+        double r = 0.0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {  // workgroups in increasing order per lane pair
-            const unsigned o = __shfl_xor(v[k], 1, 64);
-            const unsigned lo = (lane & 1) ? o : v[k], hi = (lane & 1) ? v[k] : o;
-            if (!(lane & 1) && c0 + lane + 64 * k < 2 * G)
-                acc = acc + __longlong_as_double((long long)(((u64)hi << 32) | lo));
+        for (int q = 0; q < RES_NG; ++q) {  // group order, the same instructions in every workgroup
+            const unsigned lo = __builtin_amdgcn_readlane(d, 2 * q), hi = __builtin_amdgcn_readlane(d, 2 * q + 1);
+            const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
+            r = (q == 0) ? v : r + v;
         }
+        acc = all_ok ? r : 0.0;
+    } else {
+        // Lane L holds granule L + 64k of each 512-granule sweep: the lo (even L)
+        // or hi (odd L) half of workgroup c0/2 + L/2 + 32k.
+        for (int c0 = 0; c0 < 2 * G && all_ok; c0 += 512) {
+            unsigned v[8];
+            for (;;) {
+                // All 8 loads unconditionally (out-of-range lanes re-read granule 0
+                // and ignore it): a per-load bounds branch made the compiler wait for
+                // each load before issuing the next -- 8 serial round trips to the
+                // point of coherence per poll instead of one.
+                u64 x[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int g = c0 + lane + 64 * k;
+                    x[k] = __hip_atomic_load(slot + (g < 2 * G ? g : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const bool in = c0 + lane + 64 * k < 2 * G;
+                    v[k] = in ? (unsigned)x[k] : 0u;
+                    ok = ok && (!in || (unsigned)(x[k] >> 32) == tag);
+                }
+                if (__all(ok)) break;
+                if (wall_clock64() > deadline) {
+                    all_ok = false;
+                    int miss = 0x7FFF;  // the lowest workgroup whose granule never came
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int g = c0 + lane + 64 * k;
+                        if (g < 2 * G && (unsigned)(__hip_atomic_load(slot + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                    >> 32) != tag)
+                            miss = min(miss, g >> 1);
+                    }
+                    for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, 64));
+                    if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(RES_POLL_SLEEP);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {  // workgroups in increasing order per lane pair
+                const unsigned o = __shfl_xor(v[k], 1, 64);
+                const unsigned lo = (lane & 1) ? o : v[k], hi = (lane & 1) ? v[k] : o;
+                if (!(lane & 1) && c0 + lane + 64 * k < 2 * G)
+                    acc = acc + __longlong_as_double((long long)(((u64)hi << 32) | lo));
+            }
+        }
+        acc = wave_sum(acc);  // butterfly: the same value on every lane of every workgroup
     }
-    acc = wave_sum(acc);  // butterfly: the same value on every lane of every workgroup
     if (all_ok && a.nranks > 1) {
         const unsigned seq = a.xseq0 + 1u + (unsigned)p, par = seq & 1u;
         if (blockIdx.x == 0 && lane < 2 * a.nranks) {
@@ -1384,7 +1482,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
-        if (t < 64) res_exchange(a, xi, sm, bc, &okf);
+        if (t < 64) res_exchange<RWAVES, CW>(a, xi, sm, bc, &okf);
         __syncthreads();
         ++xi;
         h = bc[0];
@@ -1514,7 +1612,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                     if (c0 + k < cend) X[k] = ldv<NT>(colchunk(q2, c0 + k) + td);
             }
         }
-        if (t < 64) res_exchange(a, xi, sm, bc, &okf);
+        if (t < 64) res_exchange<RWAVES, CW>(a, xi, sm, bc, &okf);
         __syncthreads();
         ++xi;
         h = bc[0];
