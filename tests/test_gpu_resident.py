@@ -49,6 +49,11 @@ CASES = [
     (256, 40, "cheb", 12, 16),       # two-array variant (+ LDS-resident w)
     (200, 25, "identity", 4, 32),    # R2 = 4 with a streamed part
     (512, 30, "identity", 8, 4),     # R2 = 8, fully resident
+    # even spread of the resident chunks (ResPlan::r2e / l2e): register part and
+    # LDS part only partly used, as at 2048^2 with every CU
+    (1024, 10, "identity", 0, 2),    # auto variant, 128 workgroups
+    (700, 12, "cbpr2", 12, 4),       # two-array variant, LDS part partly filled
+    (2048, 8, "identity", 0, 1),     # the size whose contiguous fill idled 70 % of the workgroups
 ]
 
 
