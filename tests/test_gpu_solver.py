@@ -60,9 +60,21 @@ def test_mgsr_128_identity_matches_reference(oracle):
     assert np.max(np.abs(r.x - 1.0)) < 1e-9
     ref = oracle.gmres_mgsr(oracle.rhs_ones(128), 128, 30, variant=oracle.MGSR_OMP)
     _hist_close(r.hist_res, ref.hist_res)
-    # final_err of the last cycle, step by step
-    k = min(r.n_out, ref.n_out)
-    assert np.allclose(r.final_err[:k], ref.final_err[:k], rtol=1e-2, atol=1e-15)
+    # the last cycle differs between runs that end a few iterations apart (3592 vs
+    # 3587-3589 in the reference itself): its final_err is compared at a fixed
+    # cycle count below (test_mgsr_128_final_err_fixed_cycles)
+
+
+def test_mgsr_128_final_err_fixed_cycles(oracle):
+    """final_err(1:m) step by step and the per-cycle residuals after exactly 3
+    cycles (config 1): the oracle against itself at 1 vs 2/4/8 OpenMP threads
+    differs by <= 1.5e-14 relative in final_err and 8.6e-15 in the residuals;
+    the tree-reduced device dots get 1e-10."""
+    r = _solve(128, 30, "identity", max_cycles=3)
+    ref = oracle.gmres_mgsr(oracle.rhs_ones(128), 128, 30, variant=oracle.MGSR_OMP, max_cycles=3)
+    assert r.n_out == ref.n_out == 30 and r.n_cycles == 3 and len(r.hist_res) == len(ref.hist_res)
+    assert np.allclose(r.final_err[:30], ref.final_err[:30], rtol=1e-10, atol=0)
+    assert np.allclose(r.hist_res, ref.hist_res, rtol=1e-10, atol=0)
 
 
 def test_mgsr_128_mf_variant(oracle):
@@ -292,12 +304,30 @@ def test_chebyshev_with_lanczos_interval_converges():
     assert np.max(np.abs(r.x - 1.0)) < 1e-9
 
 
+@pytest.mark.parametrize("solver,prec", [("pcg", "identity"), ("pcg", "cbpr2"), ("pbicgstab", "identity"),
+                                         ("pbicgstab", "cbpr2")])
+def test_short_recurrence_solvers_vs_reference_run(solver, prec):
+    """pcg_omp / pbicgstab_omp against the reference's own runs (48^2, tol 1e-9,
+    tests/golden/reference_runs.json): iteration count (PCG +-2, BiCGSTAB +-15 %,
+    its recurrence amplifies reduction-order differences) and convergence."""
+    import gmres_amd as ga
+
+    g = json.load(open(os.path.join(HERE, "golden", "reference_runs.json")))[f"{solver}_omp_{prec}_48"]
+    with ga.Context(48, 8) as ctx:
+        ctx.set_precond(prec, (8.2, 0.2), 4)
+        ctx.set_rhs_ones()
+        x, it, res, _ = getattr(ga, solver)(ctx, 1e-9, g["m"], want_hist=True)
+    assert res < 1e-9 and g["res"] < 1e-9
+    assert abs(it - g["iterations"]) <= (2 if solver == "pcg" else max(3, 0.15 * g["iterations"])), (it, g["iterations"])
+    assert np.max(np.abs(x - 1.0)) < 1e-6
+
+
 @pytest.mark.parametrize("solver", ["pcg", "pbicgstab"])
 @pytest.mark.parametrize("prec", ["identity", "cbpr2", "cheb"])
 def test_short_recurrence_solvers_vs_oracle(oracle, solver, prec):
     """pcg_omp / pbicgstab_omp on the same device kernels,
-    against the oracle restatement (no recorded reference output exists for
-    these drivers: parity vs the restatement only)."""
+    against the oracle restatement -- which reproduces the reference's own runs
+    bit for bit (tests/test_reference.py); Chebyshev(k) is build-defined."""
     import gmres_amd as ga
 
     N, tol = 64, 1e-9
