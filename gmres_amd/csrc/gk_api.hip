@@ -760,7 +760,7 @@ int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 //  RES_HH_UP: w = P_j..P_1 w (pin = <w, P_1>); hs[0] = ||w(j+1:n)||^2.
 //  RES_HH_DOWN: w = P_1..P_j w (no pin).
 int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, double *hs, double *hcopy,
-             int mode = gk::RES_MGS, double *w = nullptr) {
+             int mode = gk::RES_MGS, double *w = nullptr, i64 unit_g = -1) {
     ProfScope ps(c, GK_KID_RES);
     const int np = mode == gk::RES_MGS ? 2 * j : j;  // exchanges of the launch
     if (c->res_tag > 0xF0000000u) {  // tags must never repeat within the granule region's lifetime
@@ -785,6 +785,8 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
     a.nres2 = p.nres2;
     a.r2e = p.r2e;
     a.l2e = p.l2e;
+    a.unit_known = mode == gk::RES_HH_DOWN && unit_g >= 0;
+    a.unit_e = (a.unit_known && unit_g >= c->g0 && unit_g < c->g0 + c->nloc) ? unit_g - c->g0 : -1;
     a.tag0 = c->res_tag;
     c->res_tag += (unsigned)np;
     a.timeout = (gk::u64)c->res_timeout_ms * (gk::u64)c->xs_tick_per_ms;
@@ -850,8 +852,21 @@ template <typename K>
 dim3 cf_grid(gk_ctx *c, K kern, int L, int &JT) {
     const int H = L + (L & 1);
     const int gx = (c->N + (gk::CF_PTS - 2 * H) - 1) / (gk::CF_PTS - 2 * H);
+    // the occupancy query once per (kernel, device): every Arnoldi step launches a pass
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<const void *, int>, int>> seen;
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, gk::CF_W, 0) != hipSuccess || occ <= 0) occ = 8;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        const auto key = std::make_pair(reinterpret_cast<const void *>(kern), c->dev);
+        for (const auto &e : seen)
+            if (e.first == key) occ = e.second;
+        if (occ == 0) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, gk::CF_W, 0) != hipSuccess || occ <= 0)
+                occ = 8;
+            seen.emplace_back(key, occ);
+        }
+    }
     const i64 cap = (i64)occ * std::max(1, c->res_cus > 0 ? c->res_cus : 256);
     static const int jts[] = {16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 256, 384, 512, 1024, 2048, 4096, 8192};
     // sized by the largest slab, so every rank writes the same number of
@@ -1116,10 +1131,14 @@ int gram(gk_ctx *c, const double *base, int ncols, std::vector<double> &G) {
 
 // v <- P_1 .. P_k v  (apply reflections k..1; hh_step :269-283, update :361-373,
 // calculate_verr :581-585).  The chain's first launch is a pure dot.
-int reflect_chain_down(gk_ctx *c, double *v, int k) {
+// unit_g >= 0: v is the unit vector e at global index unit_g (gk_hh_step's v_j,
+// calculate_verr's columns), so the chain's leading dot <e, P_k> is the single
+// element P_k(unit_g) -- exactly what the full dot sums to -- and the resident
+// launch skips that pass.
+int reflect_chain_down(gk_ctx *c, double *v, int k, i64 unit_g = -1) {
     double *P = c->V;
     ResPlan rp;
-    if (res_plan(c, rp)) return res_step(c, k, rp, nullptr, 0, nullptr, nullptr, gk::RES_HH_DOWN, v);
+    if (res_plan(c, rp)) return res_step(c, k, rp, nullptr, 0, nullptr, nullptr, gk::RES_HH_DOWN, v, unit_g);
     int s0 = 0, s1 = 1;
     CHK(proj(c, gk::PJ_DOT, v, nullptr, P + (i64)(k - 1) * c->ld, nullptr, 0, slot(c, s0), nullptr, 2.0));
     int np = c->np_pj;
@@ -1817,7 +1836,7 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
         gk::k_set_unit<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->vj, c->nloc, c->g0, j - 1, 1.0);
         LAUNCHCHK();
     }
-    CHK(reflect_chain_down(c, c->vj, j));
+    CHK(reflect_chain_down(c, c->vj, j, j - 1));
     // w = M^-1 A v_j (or A v_j), fused with <w, P_1>
     int s0 = 0, s1 = 1;
     if (precondition) {
@@ -1913,7 +1932,7 @@ int gk_hh_verr(gk_ctx *c, int n_out, double *v_err) {
         double *col = c->Vb + (i64)(i - 1) * c->ld;
         gk::k_set_unit<<<c->nblk_stream, gk::TPB, 0, c->st>>>(col, c->nloc, c->g0, i - 1, 1.0);
         LAUNCHCHK();
-        if (!verr_ref_order(c)) CHK(reflect_chain_down(c, col, i));
+        if (!verr_ref_order(c)) CHK(reflect_chain_down(c, col, i, i - 1));
     }
     if (verr_ref_order(c)) {  // :581-585 with the reference's dots, all chains level by level
         CHK(ensure_gram(c, n_out));

@@ -1101,6 +1101,8 @@ struct ResArgs {
     unsigned tag0;        // granule tag of exchange p = tag0 + p (never 0)
     int j;
     i64 n, nres2;         // local length; resident double2 prefix
+    i64 unit_e;           // RES_HH_DOWN with unit_known: local index of the input's 1.0 (-1: other rank)
+    int unit_known;       // the input vector is a unit vector: leading dot = one element, no pass
     int r2e, l2e;         // chunks per workgroup actually resident in registers / LDS (<= the
                           // template's R2 / L2): the resident prefix is spread evenly
     XsPeers peers;        // nranks > 1: device exchange regions
@@ -1458,7 +1460,9 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         const int q = res_col(mode, j, 0);
         const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
         double acc = 0.0;
-        if (data) {
+        if (a.unit_known) {  // <e_u, P_q> = P_q(u): the one nonzero product, as the full sum gives it
+            if (blockIdx.x == 0 && t == 0 && a.unit_e >= 0) acc = a.V[(i64)q * a.ld + a.unit_e];
+        } else if (data) {
 #pragma unroll
             for (int k = 0; k < R2; ++k) {
                 acc = acc + wr[k].x * xa[k].x;
@@ -1894,7 +1898,12 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         // unrolled register loop would not fit the register file
         const int q = res_col(mode, j, 0);
         if (XPF) load_first(q, q, true);
-        const double acc = pass(0.0, q, q, RK_DOT);
+        double acc = 0.0;
+        if (a.unit_known) {  // <e_u, P_q> = P_q(u): the one nonzero product, as the full sum gives it
+            if (blockIdx.x == 0 && t == 0 && a.unit_e >= 0) acc = a.V[(i64)q * a.ld + a.unit_e];
+        } else {
+            acc = pass(0.0, q, q, RK_DOT);
+        }
         if (XPF) load_first(q, res_col(mode, j, 1), kind_of(0) == RK_DOT);
         ok = reduce(acc, h, kind_of(0) == RK_DOT ? res_col(mode, j, 1) : -1);
     } else {
