@@ -25,6 +25,7 @@ GK_ERR_COMM = -6
 GK_TUNE_XCHG_TIMEOUT_MS = 7
 GK_TUNE_RES, GK_TUNE_RES_R2, GK_TUNE_RES_SHARE, GK_TUNE_RES_TIMEOUT_MS = 8, 9, 10, 11
 GK_TUNE_VERR_ORDER = 14
+GK_TUNE_HH_FUSE = 15
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES = range(7)
 KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res"]
@@ -94,6 +95,7 @@ _SIGS = {
     "gk_profile_read": (c_int, [c_vp, c_int, _dp, ctypes.POINTER(c_ll)]),
     "gk_sync": (c_int, [c_vp]),
     "gk_profile_res_wg": (c_int, [c_vp, c_int, _dp, _dp, c_int, _ip]),
+    "gk_profile_res_trace": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, _ip, _ip, _dp]),
     "gk_profile_res_split": (c_int, [c_vp, c_int, c_int, _dp, _dp, _dp, ctypes.POINTER(c_ll)]),
     "gk_set_tuning": (c_int, [c_vp, c_int, c_int]),
     "gk_lanczos_bounds": (c_int, [c_vp, c_int, _dp, _dp]),

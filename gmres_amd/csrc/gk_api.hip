@@ -137,11 +137,15 @@ struct gk_ctx {
     int tune_res_lds = 1;                           // LDS-resident part of w for large slabs
     int tune_res_wonly = -1;                        // large slabs: w-only variant (-1: by the byte model)
     int tune_verr_order = 1;                        // v_err diagnostics in the reference's dot order
+    int tune_hh_fuse = 1;                           // Householder step: small launches folded into the chains
     int res_share = 1;                              // contexts sharing this device's CUs
     int res_timeout_ms = 20000;
     bool res_broken = false;                        // a deadline was missed: launch path from then on
     gk::u64 *res_stamps = nullptr;                  // gk_profile_res_split: [RGMAX][4] ticks per workgroup
     bool res_split = false;
+    gk::u64 *res_trace = nullptr;                   // gk_profile_res_trace: [RGMAX][RES_TRACE_X][2] ticks
+    int res_trace_j = 0, res_trace_mode = -1;       // the traced launch: step j, mode (-1 = off)
+    int res_trace_g = 0, res_trace_np = 0;          // its workgroups and exchanges
     // launch geometry
     int vec = 2, JT = 16;
     dim3 sgrid;
@@ -759,10 +763,16 @@ int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 //    (all-reduced) partial slab of the first dot <w, V(:,1)>; H column to hs/hcopy.
 //  RES_HH_UP: w = P_j..P_1 w (pin = <w, P_1>); hs[0] = ||w(j+1:n)||^2.
 //  RES_HH_DOWN: w = P_1..P_j w (no pin).
+//  flags (w-only variant, p.wo): RESF_CLOSE_HH -- RES_HH_UP also makes P(:,j+1) and
+//    writes w(1:j+1) to c->hb (one more exchange); RESF_UNIT_INIT -- RES_HH_DOWN builds
+//    its unit input e_{unit_g} itself.
+enum { RESF_CLOSE_HH = 1, RESF_UNIT_INIT = 2 };
 int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, double *hs, double *hcopy,
-             int mode = gk::RES_MGS, double *w = nullptr, i64 unit_g = -1) {
+             int mode = gk::RES_MGS, double *w = nullptr, i64 unit_g = -1, int flags = 0) {
     ProfScope ps(c, GK_KID_RES);
-    const int np = mode == gk::RES_MGS ? 2 * j : j;  // exchanges of the launch
+    const bool close = (flags & RESF_CLOSE_HH) && mode == gk::RES_HH_UP;
+    if (flags != 0 && !p.wo) return set_err(GK_ERR_STATE, "resident flags %d need the w-only variant", flags);
+    const int np = (mode == gk::RES_MGS ? 2 * j : j) + (close ? 1 : 0);  // exchanges of the launch
     if (c->res_tag > 0xF0000000u) {  // tags must never repeat within the granule region's lifetime
         HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_WORDS, c->st));
         c->res_tag = 1;
@@ -787,11 +797,19 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
     a.l2e = p.l2e;
     a.unit_known = mode == gk::RES_HH_DOWN && unit_g >= 0;
     a.unit_e = (a.unit_known && unit_g >= c->g0 && unit_g < c->g0 + c->nloc) ? unit_g - c->g0 : -1;
+    a.unit_init = a.unit_known && (flags & RESF_UNIT_INIT) ? 1 : 0;
+    a.close_hh = close ? 1 : 0;
+    a.hb = c->hb;
     a.tag0 = c->res_tag;
     c->res_tag += (unsigned)np;
     a.timeout = (gk::u64)c->res_timeout_ms * (gk::u64)c->xs_tick_per_ms;
     a.err = c->res_err_dev;
     a.stamps = c->res_split ? c->res_stamps : nullptr;
+    if (c->res_trace != nullptr && j == c->res_trace_j && mode == c->res_trace_mode) {
+        a.trace = c->res_trace;
+        c->res_trace_g = p.G;
+        c->res_trace_np = np;
+    }
     a.nranks = 1;
     if (c->xs_on && c->nranks > 1) {
         a.err = c->xs_err_dev;
@@ -1135,10 +1153,12 @@ int gram(gk_ctx *c, const double *base, int ncols, std::vector<double> &G) {
 // calculate_verr's columns), so the chain's leading dot <e, P_k> is the single
 // element P_k(unit_g) -- exactly what the full dot sums to -- and the resident
 // launch skips that pass.
-int reflect_chain_down(gk_ctx *c, double *v, int k, i64 unit_g = -1) {
+int reflect_chain_down(gk_ctx *c, double *v, int k, i64 unit_g = -1, int flags = 0) {
     double *P = c->V;
     ResPlan rp;
-    if (res_plan(c, rp)) return res_step(c, k, rp, nullptr, 0, nullptr, nullptr, gk::RES_HH_DOWN, v, unit_g);
+    if (res_plan(c, rp))
+        return res_step(c, k, rp, nullptr, 0, nullptr, nullptr, gk::RES_HH_DOWN, v, unit_g, flags);
+    if (flags != 0) return set_err(GK_ERR_STATE, "resident chain flags without a resident plan");
     int s0 = 0, s1 = 1;
     CHK(proj(c, gk::PJ_DOT, v, nullptr, P + (i64)(k - 1) * c->ld, nullptr, 0, slot(c, s0), nullptr, 2.0));
     int np = c->np_pj;
@@ -1254,6 +1274,7 @@ int gk_destroy(gk_ctx *c) {
     if (c->xs_err) (void)hipHostFree(c->xs_err);
     if (c->res_gath) (void)hipFree(c->res_gath);
     if (c->res_stamps) (void)hipFree(c->res_stamps);
+    if (c->res_trace) (void)hipFree(c->res_trace);
     if (c->res_err) (void)hipHostFree(c->res_err);
     double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi, c->dh,
                       c->red, c->hcol, c->ydev, c->hb, c->scal, c->Vb, c->gram_slab, c->gram_out};
@@ -1830,13 +1851,19 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
     HIPCHK(hipSetDevice(c->dev));
     const i64 ld = c->ld;
     double *P = c->V;
+    // The w-only resident variant folds the step's small launches into its chains
+    // (GK_TUNE_HH_FUSE): the DOWN chain builds e_j itself (no k_set_unit), the UP
+    // chain ends with the fix-up and P(:,j+1) = w/||w|| (no k_hh_fix, no k_scale).
+    ResPlan rp;
+    const bool res = res_plan(c, rp);
+    const bool fuse = res && rp.wo && c->tune_hh_fuse != 0;
     // v_j = e_j ; v_j = P_1 .. P_j e_j
-    {
+    if (!fuse) {
         ProfScope ps(c, GK_KID_OTHER);
         gk::k_set_unit<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->vj, c->nloc, c->g0, j - 1, 1.0);
         LAUNCHCHK();
     }
-    CHK(reflect_chain_down(c, c->vj, j, j - 1));
+    CHK(reflect_chain_down(c, c->vj, j, j - 1, fuse ? RESF_UNIT_INIT : 0));
     // w = M^-1 A v_j (or A v_j), fused with <w, P_1>
     int s0 = 0, s1 = 1;
     if (precondition) {
@@ -1851,8 +1878,22 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
         CHK(stencil(c, gk::OP_PLAIN, gk::ACC_DOT, a));
     }
     int np = c->last_np;
-    ResPlan rp;
-    if (res_plan(c, rp)) {  // w = P_j .. P_1 w and ||w(j+1:n)||^2 as one resident launch
+    if (fuse) {  // w = P_j .. P_1 w, ||w(j+1:n)||^2, the fix-up and P(:,j+1), one launch
+        CHK(allreduce(c, slot(c, s0), np));
+        CHK(res_step(c, j, rp, slot(c, s0), np, slot(c, s1), nullptr, gk::RES_HH_UP, c->w, -1, RESF_CLOSE_HH));
+        // H(1:j+1, j) from hb (written by the owner rank's launch) on every rank
+        CHK(bcast(c, c->hb, j + 1, owner_of(c, j)));
+        {
+            ProfScope ps(c, GK_KID_OTHER);
+            const int m2 = c->m + 2;
+            gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, s1), 1, j, c->hall + (i64)(j - 1) * m2,
+                                                     c->scal + 2, c->hallh_dev + (i64)(j - 1) * m2);
+            LAUNCHCHK();
+        }
+        HIPCHK(hipEventRecord(c->ev_step[j], c->st));
+        return GK_OK;
+    }
+    if (res) {  // w = P_j .. P_1 w and ||w(j+1:n)||^2 as one resident launch
         CHK(allreduce(c, slot(c, s0), np));
         CHK(res_step(c, j, rp, slot(c, s0), np, slot(c, s1), nullptr, gk::RES_HH_UP, c->w));
         std::swap(s0, s1);
@@ -2011,6 +2052,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
             break;
         case GK_TUNE_RES_LDS: c->tune_res_lds = value != 0; break;
         case GK_TUNE_RES_WONLY: c->tune_res_wonly = value < 0 ? -1 : (value != 0); break;
+        case GK_TUNE_HH_FUSE: c->tune_hh_fuse = value != 0; break;
         case GK_TUNE_VERR_ORDER: c->tune_verr_order = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
@@ -2077,6 +2119,43 @@ int gk_profile_res_wg(gk_ctx *c, int which, double *pass_ms, double *wait_ms, in
             ++g;
         }
     *nwg = g;
+    return GK_OK;
+}
+
+int gk_profile_res_trace(gk_ctx *c, int arm, int j, int mode, unsigned long long *out, int maxwg, int maxx,
+                         int *nwg, int *nx, double *tick_per_ms) {
+    CHK(check_ctx(c));
+    HIPCHK(hipSetDevice(c->dev));
+    const size_t words = (size_t)gk::RGMAX * gk::RES_TRACE_X * 2;
+    if (arm == 1) {
+        if (mode != gk::RES_MGS || j < 1) return set_err(GK_ERR_ARG, "trace: MGS-R step launches (mode 0), j >= 1");
+        if (c->res_trace == nullptr) HIPCHK(hipMalloc(&c->res_trace, sizeof(gk::u64) * words));
+        HIPCHK(hipMemsetAsync(c->res_trace, 0, sizeof(gk::u64) * words, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        c->res_trace_j = j;
+        c->res_trace_mode = mode;
+        c->res_trace_g = c->res_trace_np = 0;
+        return GK_OK;
+    }
+    if (arm == 0) {
+        c->res_trace_mode = -1;
+        return GK_OK;
+    }
+    if (out == nullptr || nwg == nullptr || nx == nullptr || tick_per_ms == nullptr || maxwg < 1 || maxx < 1)
+        return set_err(GK_ERR_ARG, "bad arguments");
+    *nwg = *nx = 0;
+    *tick_per_ms = (double)c->xs_tick_per_ms;
+    if (c->res_trace == nullptr || c->res_trace_g == 0) return GK_OK;
+    std::vector<gk::u64> h(words);
+    HIPCHK(hipMemcpyAsync(h.data(), c->res_trace, sizeof(gk::u64) * words, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    const int G = std::min(c->res_trace_g, maxwg), X = std::min({c->res_trace_np, maxx, gk::RES_TRACE_X});
+    for (int b = 0; b < G; ++b)
+        for (int x = 0; x < X; ++x)
+            for (int k = 0; k < 2; ++k)
+                out[((size_t)b * X + x) * 2 + k] = h[((size_t)b * gk::RES_TRACE_X + x) * 2 + k];
+    *nwg = G;
+    *nx = X;
     return GK_OK;
 }
 

@@ -1112,7 +1112,14 @@ struct ResArgs {
     double coef;          // AXPY coefficient: w -= (coef*h) V_i (1 for MGS, 2 for reflections)
     i64 tail0;            // RES_HH_UP: the closing norm counts local indices >= tail0
     u64 *stamps;          // profiling (nullptr = off): [mode][workgroup][pass, wait, total, launches] ticks
+    // w-only kernel (k_mgs_wres) only:
+    int close_hh;         // RES_HH_UP: the launch also makes the next reflector (gmres_hh.f90:306-318):
+                          // w(1:j) = 0, w(j+1) += sign, P(:,j+1) = w / ||w|| to vout (w not written back)
+    double *hb;           // close_hh: w(1:j+1) before the fix-up, written by the owner rank (pivot input)
+    int unit_init;        // RES_HH_DOWN with unit_known: the launch builds e_u itself (w not read)
+    u64 *trace;           // gk_profile_res_trace (nullptr = off): [workgroup][RES_TRACE_X][publish, seen] ticks
 };
+constexpr int RES_TRACE_X = 2 * RHMAX + 2;  // exchanges recorded per workgroup (all of one launch)
 
 // Time split of a resident launch (gk_profile_res_split): thread 0 of each
 // workgroup accumulates wall-clock ticks spent streaming its passes and waiting
@@ -1219,7 +1226,9 @@ constexpr i64 RES_GATH_WORDS = 4 * (i64)RGMAX + 4 * RES_NG;  // [2][RGMAX][2] pa
 // projection: continuous polls by early finishers slow the stragglers' streams.
 constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
 
-template <int NW = RWAVES, bool HOP2 = false>
+// TR: the trace stamps (gk_profile_res_trace) are compiled into the MGS-R launches only
+// (the reflection kernels are at the edge of the register file).
+template <int NW = RWAVES, bool HOP2 = false, bool TR = false>
 __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const double *sm, double *bc, int *okf) {
     const int lane = threadIdx.x;
     const int G = gridDim.x;
@@ -1228,6 +1237,8 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
     double s = sm[0];
 #pragma unroll
     for (int w = 1; w < NW; ++w) s += sm[w];
+    u64 t_pub = 0;
+    if (TR && a.trace != nullptr) t_pub = wall_clock64();
     if (lane == 0) {
         const u64 bits = (u64)__double_as_longlong(s);
         __hip_atomic_store(slot + 2 * blockIdx.x, ((u64)tag << 32) | (unsigned)bits, __ATOMIC_RELAXED,
@@ -1399,6 +1410,11 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
     if (lane == 0) {
         bc[0] = acc;
         *okf = all_ok ? 1 : 0;
+        if (TR && a.trace != nullptr && p < RES_TRACE_X) {
+            u64 *q = a.trace + ((i64)blockIdx.x * RES_TRACE_X + p) * 2;
+            q[0] = t_pub;
+            q[1] = wall_clock64();
+        }
     }
 }
 
@@ -1486,7 +1502,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
-        if (t < 64) res_exchange<RWAVES, CW>(a, xi, sm, bc, &okf);
+        if (t < 64) res_exchange<RWAVES, CW, MODE == RES_MGS>(a, xi, sm, bc, &okf);
         __syncthreads();
         ++xi;
         h = bc[0];
@@ -1616,7 +1632,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                     if (c0 + k < cend) X[k] = ldv<NT>(colchunk(q2, c0 + k) + td);
             }
         }
-        if (t < 64) res_exchange<RWAVES, CW>(a, xi, sm, bc, &okf);
+        if (t < 64) res_exchange<RWAVES, CW, MODE == RES_MGS>(a, xi, sm, bc, &okf);
         __syncthreads();
         ++xi;
         h = bc[0];
@@ -1737,13 +1753,26 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     ResClock clk;
     clk.start(a.stamps);
     int touch_sink = 0;
-    double2 wr[RW];
-#pragma unroll
-    for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
-    for (int k = 0; k < LW; ++k)
-        if (l0 + k < lend) lw[k * WT + t] = W2[(l0 + k) * WT + t];
     const i64 sstride = (i64)gridDim.x * WT;
     const i64 sbase = a.nres2 + (i64)blockIdx.x * WT + t;
+    double2 wr[RW];
+    if (mode == RES_HH_DOWN && a.unit_init) {
+        // w = e_u built in place (gmres_hh.f90:257-264): no k_set_unit launch, no read
+        // of w; the streamed part is written by the thread that streams it later
+        const i64 u = a.unit_e;  // local index of the 1.0, -1 on other ranks
+        auto unit2 = [&](i64 e2) { return double2{2 * e2 == u ? 1.0 : 0.0, 2 * e2 + 1 == u ? 1.0 : 0.0}; };
+#pragma unroll
+        for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? unit2((c0 + k) * WT + t) : double2{0.0, 0.0};
+        for (int k = 0; k < LW; ++k)
+            if (l0 + k < lend) lw[k * WT + t] = unit2((l0 + k) * WT + t);
+        for (i64 e = sbase; e < n2; e += sstride) W2[e] = unit2(e);
+        if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.w[a.n - 1] = (a.n - 1 == u) ? 1.0 : 0.0;
+    } else {
+#pragma unroll
+        for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
+        for (int k = 0; k < LW; ++k)
+            if (l0 + k < lend) lw[k * WT + t] = W2[(l0 + k) * WT + t];
+    }
     // acc += the closing reduction of element pair e2 (local double2 index)
     auto red = [&](double &acc, const double2 &v, const double2 &b, int kind, i64 e2, bool chk) {
         if (kind == RK_DOT) {
@@ -1865,7 +1894,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
         if (t < 64) {
-            res_exchange<WT / 64>(a, xi, sm, bc, &okf);
+            res_exchange<WT / 64, false, MODE == RES_MGS>(a, xi, sm, bc, &okf);
         } else if constexpr (TOUCH > 0) {
             if (touch_col >= 0) {
                 // lines [0, 32*TOUCH) of the workgroup's register-resident part of
@@ -1927,19 +1956,20 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         if (kind != RK_NONE) ok = reduce(acc, h, p + 1 < np && kind_of(p + 1) == RK_DOT ? res_col(mode, j, p + 2) : -1);
     }
     if (!ok) return;  // uniform per workgroup; *err is set
-    if (mode != RES_MGS) {  // reflections: the resident part of w back to HBM
+    const bool close = mode == RES_HH_UP && a.close_hh;
+    if (mode != RES_MGS) {  // reflections: the resident part of w back to HBM (not when close)
         double acc = 0.0;  // RES_HH_UP: ||w(j+1:n)||^2, local indices >= tail0
         const bool up = mode == RES_HH_UP;
 #pragma unroll
         for (int k = 0; k < RW; ++k)
             if (c0 + k < cend) {
-                W2[(c0 + k) * WT + t] = wr[k];
+                if (!close) W2[(c0 + k) * WT + t] = wr[k];
                 if (up) sq_acc(acc, wr[k], (c0 + k) * WT + t, tail0, c0 + k == 0);
             }
         for (int k = 0; k < LW; ++k)
             if (l0 + k < lend) {
                 const double2 v = lw[k * WT + t];
-                W2[(l0 + k) * WT + t] = v;
+                if (!close) W2[(l0 + k) * WT + t] = v;
                 if (up) sq_acc(acc, v, (l0 + k) * WT + t, tail0, l0 + k == 0);
             }
         if (up) {
@@ -1952,8 +1982,64 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             if (!ok) return;
             if (blockIdx.x == 0 && t == 0) a.hs[0] = h;  // ||w(j+1:n)||^2
         }
-        clk.finish(a.stamps, mode);
-        return;
+        if (!close) {
+            clk.finish(a.stamps, mode);
+            return;
+        }
+        // Next reflector in the same launch (gmres_hh.f90:306-318; k_hh_pivot + k_hh_fix +
+        // k_scale of the launch path, the same element arithmetic): on the rank owning
+        // w(j+1) (local index f = tail0 >= 0) H(j+1,j) = w(j+1) > 0 ? -tmp : tmp with tmp =
+        // sqrt(h), w(1:j) = 0, w(j+1) = w(j+1) - H; then P(:,j+1) = w / ||w||.  w(1:j+1)
+        // before the fix goes to hb for the pivot kernel (the H column).  The indices <= f
+        // lie in chunks 0 and 1 (f <= RHMAX): the per-element test runs there only.
+        const double s = sqrt(h);
+        const i64 f = tail0;
+        auto fix1 = [&](double &x, i64 g) {
+            if (g < f) {
+                a.hb[g] = x;
+                x = 0.0;
+            } else if (g == f) {
+                a.hb[g] = x;
+                const double dl = (x > 0.0) ? s : -s;  // delta = -H
+                x = x + dl;
+            }
+        };
+        auto fix_sq = [&](double &acc2, double2 &v, i64 e2, bool chk) {
+            if (chk) {
+                fix1(v.x, 2 * e2);
+                fix1(v.y, 2 * e2 + 1);
+            }
+            acc2 = acc2 + v.x * v.x;
+            acc2 = acc2 + v.y * v.y;
+        };
+        const i64 cfix = f >= 0 ? f / (2 * WT) : -1;  // last chunk holding an index <= f
+        double acc2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < RW; ++k)
+            if (c0 + k < cend) fix_sq(acc2, wr[k], (c0 + k) * WT + t, c0 + k <= cfix);
+        for (int k = 0; k < LW; ++k)
+            if (l0 + k < lend) {
+                double2 v = lw[k * WT + t];
+                const bool chk = l0 + k <= cfix;
+                fix_sq(acc2, v, (l0 + k) * WT + t, chk);
+                if (chk) lw[k * WT + t] = v;
+            }
+        for (i64 e = sbase; e < n2; e += sstride) {
+            double2 v = W2[e];
+            const bool chk = 2 * e <= f;
+            fix_sq(acc2, v, e, chk);
+            if (chk) W2[e] = v;
+        }
+        if ((a.n & 1) && blockIdx.x == 0 && t == 0) {
+            double x = a.w[a.n - 1];
+            if (a.n - 1 <= f) {
+                fix1(x, a.n - 1);
+                a.w[a.n - 1] = x;
+            }
+            acc2 = acc2 + x * x;
+        }
+        ok = reduce(acc2, h, -1);
+        if (!ok) return;
     }
     const double hn = sqrt(h);
     double2 *__restrict__ O2 = reinterpret_cast<double2 *>(a.vout);
@@ -1972,7 +2058,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     }
     if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     clk.finish(a.stamps, mode);
-    if (blockIdx.x == 0) {
+    if (mode == RES_MGS && blockIdx.x == 0) {
         __syncthreads();
         for (int k = t; k < j; k += WT) {
             a.hs[k] = hsh[k];

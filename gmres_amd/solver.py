@@ -292,6 +292,23 @@ class Context:
                   "gk_profile_res_wg")
         return p[: n.value], w[: n.value]
 
+    def res_trace(self, arm: int, j: int = 0, mode: int = 0):
+        """All-gather trace of one resident launch (gk_profile_res_trace): arm 1 traces the
+        MGS-R step launches of step j (mode 0), 0 stops; -1 returns
+        (publish, seen) wall-clock ms as two [workgroups, exchanges] arrays."""
+        if arm != -1:
+            nat.check(nat.hip().gk_profile_res_trace(self._h, int(arm), int(j), int(mode), None, 0, 0, None, None,
+                                                     None), "gk_profile_res_trace")
+            return None
+        maxwg, maxx = 1024, 1026
+        buf = np.zeros(maxwg * maxx * 2, dtype=np.uint64)
+        g, x, tpm = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+        nat.check(nat.hip().gk_profile_res_trace(self._h, -1, 0, 0, buf.ctypes.data, maxwg, maxx, ctypes.byref(g),
+                                                 ctypes.byref(x), ctypes.byref(tpm)), "gk_profile_res_trace")
+        t = buf[: g.value * x.value * 2].reshape(g.value, x.value, 2).astype(np.float64)
+        t0 = t[t > 0].min() if np.any(t > 0) else 0.0
+        return (t[:, :, 0] - t0) / tpm.value, (t[:, :, 1] - t0) / tpm.value
+
     def tune(self, key: int, value: int) -> None:
         """Launch-policy knob (include/gmres_hip.h GK_TUNE_*)."""
         nat.check(nat.hip().gk_set_tuning(self._h, int(key), int(value)), "gk_set_tuning")

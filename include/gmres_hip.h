@@ -237,6 +237,13 @@ int gk_profile_res_split(gk_ctx *ctx, int mode, int which, double *pass_ms, doub
 /* The same split per workgroup (blockIdx order, summed over launches): the
  * arrival skew of the in-launch all-gathers shows as the spread of pass_ms. */
 int gk_profile_res_wg(gk_ctx *ctx, int which, double *pass_ms, double *wait_ms, int maxwg, int *nwg);
+/* All-gather trace of one resident launch: for every workgroup and in-launch exchange, the
+ * wall-clock ticks at which its partial was published and at which it held the grid total
+ * (tools/res_trace.py: arrival skew vs propagation).  arm 1: trace the MGS-R step launches
+ * of Arnoldi step j from now on (mode must be 0; each overwrites the last); 0: off; -1: read
+ * the last traced launch into out[nwg][nx][2]. */
+int gk_profile_res_trace(gk_ctx *ctx, int arm, int j, int mode, unsigned long long *out, int maxwg, int maxx,
+                         int *nwg, int *nx, double *tick_per_ms);
 int gk_sync(gk_ctx *ctx);
 
 /* Launch-policy knobs (defaults are the tuned values; for A/B measurement).
@@ -273,7 +280,12 @@ int gk_sync(gk_ctx *ctx);
  *   GK_TUNE_VERR_ORDER     1 (default): the v_err diagnostics (gk_mgs_verr, gk_hh_verr) use the
  *                          reference's dot_product order, one running sum per dot (bit-identical
  *                          to the reference's formula on the same basis; single rank); 0: tree
- *                          reduction (fast; N ranks always use it) */
+ *                          reduction (fast; N ranks always use it)
+ *   GK_TUNE_HH_FUSE        1 (default): with the w-only resident variant a Householder step folds
+ *                          its small launches into the reflection chains -- the DOWN chain builds
+ *                          e_j itself, the UP chain ends with the reflector fix-up and
+ *                          P(:,j+1) = w/||w|| (gmres_hh.f90:306-318); 0: separate k_set_unit,
+ *                          k_hh_fix and k_scale launches */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
@@ -289,6 +301,7 @@ int gk_sync(gk_ctx *ctx);
 #define GK_TUNE_RES_LDS 12
 #define GK_TUNE_RES_WONLY 13
 #define GK_TUNE_VERR_ORDER 14
+#define GK_TUNE_HH_FUSE 15
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

@@ -19,11 +19,13 @@ pytestmark = pytest.mark.gpu
 T_RES, T_R2, T_SHARE, T_TMO = 8, 9, 10, 11
 
 
-def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False, wonly=-1, method="mgsr"):
+def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False, wonly=-1, method="mgsr",
+         hh_fuse=1):
     import gmres_amd as ga
 
     with ga.Context(N, m) as c:
         c.tune(T_RES, res)
+        c.tune(15, hh_fuse)  # GK_TUNE_HH_FUSE
         c.tune(13, wonly)  # GK_TUNE_RES_WONLY
         c.tune(T_R2, r2)
         c.tune(T_SHARE, share)
@@ -149,3 +151,23 @@ def test_resident_householder_vs_oracle_to_convergence(oracle):
     rtol = np.where(r > 1e-6, 1e-8, np.where(r > 1e-12, 1e-3, 5e-2))
     assert np.all(np.abs(g - r) <= rtol * r + 1e-16)
     assert np.max(np.abs(got.x - 1.0)) < 1e-9
+
+
+@pytest.mark.parametrize("N,m,prec,r2,share", [(300, 20, "identity", 12, 64), (181, 16, "cbpr2", 12, 128),
+                                               (512, 30, "identity", 12, 16)])
+def test_householder_fused_step_matches_unfused(N, m, prec, r2, share):
+    """GK_TUNE_HH_FUSE: with the w-only variant the DOWN chain builds e_j in place (no
+    k_set_unit) and the UP chain ends with the reflector fix-up and P(:,j+1) = w/||w||
+    (gmres_hh.f90:306-318) instead of k_hh_fix + k_scale.  The element arithmetic is the
+    same; only ||w||^2 of the fixed vector is summed in another order, so the histories
+    agree to reduction-order noise, and the fused step runs none of the folded launches."""
+    ref, pr = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True, wonly=1, method="hh", hh_fuse=0)
+    got, pg = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True, wonly=1, method="hh", hh_fuse=1)
+    assert got.n_cycles == ref.n_cycles and got.iterations == ref.iterations
+    h, r = got.hist_res, ref.hist_res
+    tol = np.where(r > 1e-6, 1e-10, np.where(r > 1e-12, 1e-4, 5e-2))
+    assert np.all(np.abs(h - r) <= tol * r + 1e-16), (h, r)
+    k = min(got.n_out, ref.n_out)
+    assert np.allclose(got.final_err[:k], ref.final_err[:k], rtol=1e-6, atol=1e-16)
+    # per step the unfused path launches k_set_unit + k_hh_fix ("other") and k_scale
+    assert pg["scale"][1] < pr["scale"][1] and pg["other"][1] < pr["other"][1], (pg, pr)

@@ -89,10 +89,13 @@ def test_oracle_1024_threaded_vs_reference(oracle, key, rtol):
     1e-10 for Householder (measured 1.4e-11 .. 4.4e-11 at cycle 3 over repeated
     8-thread runs: the threaded reductions are not run-to-run deterministic on
     either side, and the reference's own HH and MGS-R runs differ by 1.6e-11
-    there)."""
+    there).  The first two of the fixture's three cycles are checked, to keep the
+    CPU suite within a few minutes (the three-cycle bit-exact claim is the serial
+    test above)."""
     g = REF[key]
-    r = _oracle_run(oracle, g, threads=8, max_cycles=3)
-    assert np.allclose(r.hist_res, g["hist_res"], rtol=rtol, atol=0)
+    r = _oracle_run(oracle, g, threads=8, max_cycles=2)
+    assert len(r.hist_res) == 2
+    assert np.allclose(r.hist_res, g["hist_res"][:2], rtol=rtol, atol=0)
 
 
 @pytest.mark.parametrize("key", ["mgsr_omp_identity_128_m30_t8", "hh_omp_identity_128_m30_t8"])
