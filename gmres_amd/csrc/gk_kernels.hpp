@@ -1206,44 +1206,73 @@ __device__ __forceinline__ double block_sum_rt(double v, double *sm) {
 // fixed order; on N ranks then add the rank totals in rank order.  Result in
 // bc[0]; *okf = 0 when a deadline passed (then *err is set).
 #ifndef GK_RES_XHOPS
-#define GK_RES_XHOPS 2
+#define GK_RES_XHOPS 1
 #endif
 // 1: every workgroup sweeps all partials; 2: via group leaders, in the
-// small-grid kernel (k_mgs_res with a control wave) only.  A/B
-// (profiles/r02/ab_hops_*.jsonl): two hops 4.25 vs 4.37 us per projection at
-// 1024^2, but 10.9 vs 10.4 at 2048^2 and 43.2 vs 41.6 at 4096^2, where the
-// flat sweep is not the congested part and the second round trip costs.
+// small-grid kernel (k_mgs_res with a control wave) only.  A/B with one granule
+// array (profiles/r02/ab_hops_*.jsonl): two hops 4.25 vs 4.37 us per projection at
+// 1024^2 (256 readers of one array congested the flat sweep), but 10.9 vs 10.4 at
+// 2048^2 and 43.2 vs 41.6 at 4096^2.  With 8 replicas (RES_NREP) the flat sweep
+// wins at 1024^2 too: 3.85 vs 4.1 us (profiles/r02/ab_nrep_1024.jsonl).
 constexpr int RES_XHOPS = GK_RES_XHOPS;
 constexpr int RES_NG = 8;                     // groups of the two-hop all-gather (blockIdx % 8)
 constexpr int RES_MK = (2 * RGMAX / RES_NG + 63) / 64;  // granule loads per lane of a leader's sweep
-constexpr i64 RES_GATH_WORDS = 4 * (i64)RGMAX + 4 * RES_NG;  // [2][RGMAX][2] partials + [2][NG][2] group sums
+#ifndef GK_RES_NREP
+#define GK_RES_NREP 8
+#endif
+// Replicas of the granule array: every workgroup publishes its partial into all
+// RES_NREP copies (one store per lane of 2 * NREP lanes) and sweeps copy
+// blockIdx % NREP -- under round-robin dispatch the copy of its own XCD, never
+// assumed for correctness -- so each copy's lines are polled by 1/NREP of the
+// grid instead of all of it (MI355X_MICROARCH.md allgather: 256 -> 32 readers
+// -1.9 us on a 16 KB sweep).  Copies RES_REP_STRIDE words apart (a 256 B skew on
+// top of the array size, so they fall on different channels).  1 = one array.
+constexpr int RES_NREP = GK_RES_NREP;
+constexpr i64 RES_REP_STRIDE = 4 * (i64)RGMAX + 32;
+constexpr i64 RES_REP0 = 4 * (i64)RGMAX + 4 * RES_NG;  // first replica (RES_NREP > 1)
+// [2][RGMAX][2] partials + [2][NG][2] group sums + the replicas
+constexpr i64 RES_GATH_WORDS = RES_REP0 + (RES_NREP > 1 ? RES_NREP * RES_REP_STRIDE : 0);
+// rank totals of the resident launches: replica r in value slot XS_REP_STEP * r (128 B apart)
+constexpr int XS_REP_STEP = 8;
+static_assert(RES_NREP >= 1 && RES_NREP * XS_REP_STEP <= XS_MAXV, "replicas must fit the exchange value slots");
 
 #ifndef GK_RES_POLL_SLEEP
 #define GK_RES_POLL_SLEEP 16
 #endif
-// s_sleep units (64 clocks) between unanswered polls.  A/B (profiles/r02/ab_poll_*.jsonl):
-// 1 / 4 / 16 / 48 -> 4096^2 42.1 / 42.1 / 41.7 / 41.6 us, 1024^2 4.42 / 4.45 / 4.40 / 4.81 us per
-// projection: continuous polls by early finishers slow the stragglers' streams.
+#ifndef GK_RES_POLL_SLEEP_SMALL
+#define GK_RES_POLL_SLEEP_SMALL 4
+#endif
+// s_sleep units (64 clocks) between unanswered polls, per kernel: the w-only
+// large-slab kernel (RES_POLL_SLEEP) and k_mgs_res (RES_POLL_SLEEP_SMALL).  A/B with
+// one granule array (profiles/r02/ab_poll_*.jsonl): 1 / 4 / 16 / 48 -> 4096^2 42.1 / 42.1
+// / 41.7 / 41.6 us, 1024^2 4.42 / 4.45 / 4.40 / 4.81 us per projection: continuous polls
+// by early finishers slow the stragglers' streams.  With 8 replicas
+// (profiles/r02/ab_rep_*.jsonl) 4 instead of 16: 4096^2 41.8 vs 41.5 us, but 2048^2 9.57
+// vs 9.66 and 1024^2 4.12 vs 4.28 -- a poll is cheaper once 32 readers share a copy.
 constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
+constexpr int RES_POLL_SLEEP_SMALL = GK_RES_POLL_SLEEP_SMALL;
 
 // TR: the trace stamps (gk_profile_res_trace) are compiled into the MGS-R launches only
 // (the reflection kernels are at the edge of the register file).
-template <int NW = RWAVES, bool HOP2 = false, bool TR = false>
+template <int NW = RWAVES, bool HOP2 = false, bool TR = false, int SLEEP = RES_POLL_SLEEP>
 __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const double *sm, double *bc, int *okf) {
     const int lane = threadIdx.x;
     const int G = gridDim.x;
     const unsigned tag = a.tag0 + (unsigned)p;
-    u64 *slot = a.gath + (i64)(p & 1) * G * 2;
+    auto rep_slot = [&](int r) -> u64 * {  // granule array of exchange p in replica r
+        return a.gath + (RES_NREP > 1 ? RES_REP0 + r * RES_REP_STRIDE : 0) + (i64)(p & 1) * G * 2;
+    };
+    u64 *slot = rep_slot((int)(blockIdx.x % RES_NREP));  // the copy this workgroup sweeps
     double s = sm[0];
 #pragma unroll
     for (int w = 1; w < NW; ++w) s += sm[w];
     u64 t_pub = 0;
     if (TR && a.trace != nullptr) t_pub = wall_clock64();
-    if (lane == 0) {
+    if (lane < 2 * RES_NREP) {  // lane 2r + h: half h of the partial into replica r
         const u64 bits = (u64)__double_as_longlong(s);
-        __hip_atomic_store(slot + 2 * blockIdx.x, ((u64)tag << 32) | (unsigned)bits, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(slot + 2 * blockIdx.x + 1, ((u64)tag << 32) | (unsigned)(bits >> 32), __ATOMIC_RELAXED,
+        const int half = lane & 1;
+        __hip_atomic_store(rep_slot(lane >> 1) + 2 * blockIdx.x + half,
+                           ((u64)tag << 32) | (half ? (unsigned)(bits >> 32) : (unsigned)bits), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
     const u64 deadline = wall_clock64() + a.timeout;
@@ -1290,7 +1319,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
                     if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(RES_POLL_SLEEP);
+                __builtin_amdgcn_s_sleep(SLEEP);
             }
             double gsum = 0.0;
 #pragma unroll
@@ -1322,7 +1351,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
                 if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);  // the leader of the missing group
                 break;
             }
-            __builtin_amdgcn_s_sleep(RES_POLL_SLEEP);
+            __builtin_amdgcn_s_sleep(SLEEP);
         }
         double r = 0.0;
 #pragma unroll
@@ -1370,7 +1399,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
                     if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(RES_POLL_SLEEP);
+                __builtin_amdgcn_s_sleep(SLEEP);
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {  // workgroups in increasing order per lane pair
@@ -1383,18 +1412,25 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
         acc = wave_sum(acc);  // butterfly: the same value on every lane of every workgroup
     }
     if (all_ok && a.nranks > 1) {
+        // Rank totals: workgroup 0 pushes this rank's total into every peer's region,
+        // once per replica (value slot XS_REP_STEP * r of its source row: a line of its
+        // own), and every workgroup reads replica blockIdx % NREP -- 1/NREP of the grid
+        // polls each line instead of all of it.  A slot is rewritten two exchanges later
+        // at the earliest, after every workgroup of every rank has read it (rendezvous).
         const unsigned seq = a.xseq0 + 1u + (unsigned)p, par = seq & 1u;
-        if (blockIdx.x == 0 && lane < 2 * a.nranks) {
-            const int dst = lane >> 1, half = lane & 1;
+        if (blockIdx.x == 0) {
             const u64 bits = (u64)__double_as_longlong(acc);
-            xs_put(a.peers.p[dst] + (((i64)par * XS_MAXR + a.rank) * XS_MAXV) * 2 + half, seq,
-                   half ? (unsigned)(bits >> 32) : (unsigned)bits);
+            for (int k = lane; k < 2 * RES_NREP * a.nranks; k += 64) {
+                const int dst = k / (2 * RES_NREP), r = (k >> 1) % RES_NREP, half = k & 1;
+                xs_put(a.peers.p[dst] + (((i64)par * XS_MAXR + a.rank) * XS_MAXV + XS_REP_STEP * r) * 2 + half, seq,
+                       half ? (unsigned)(bits >> 32) : (unsigned)bits);
+            }
         }
         unsigned d = 0;
         bool ok2 = true;
         if (lane < 2 * a.nranks) {
-            const int src = lane >> 1, half = lane & 1;
-            ok2 = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV) * 2 + half, seq,
+            const int src = lane >> 1, half = lane & 1, r = (int)(blockIdx.x % RES_NREP);
+            ok2 = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV + XS_REP_STEP * r) * 2 + half, seq,
                          wall_clock64() + a.timeout, &d);
             if (!ok2) xs_fail(a.err, XSE_RES_RANK, src);
         }
@@ -1502,7 +1538,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
-        if (t < 64) res_exchange<RWAVES, CW, MODE == RES_MGS>(a, xi, sm, bc, &okf);
+        if (t < 64) res_exchange<RWAVES, CW, MODE == RES_MGS, RES_POLL_SLEEP_SMALL>(a, xi, sm, bc, &okf);
         __syncthreads();
         ++xi;
         h = bc[0];
@@ -1632,7 +1668,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                     if (c0 + k < cend) X[k] = ldv<NT>(colchunk(q2, c0 + k) + td);
             }
         }
-        if (t < 64) res_exchange<RWAVES, CW, MODE == RES_MGS>(a, xi, sm, bc, &okf);
+        if (t < 64) res_exchange<RWAVES, CW, MODE == RES_MGS, RES_POLL_SLEEP_SMALL>(a, xi, sm, bc, &okf);
         __syncthreads();
         ++xi;
         h = bc[0];
@@ -1732,6 +1768,14 @@ constexpr bool XPF = XPF_MODE != 0;
 #define GK_RES_TOUCH 32
 #endif
 constexpr int TOUCH = GK_RES_TOUCH;
+#ifndef GK_RES_TOUCH_PACE
+#define GK_RES_TOUCH_PACE 0
+#endif
+// TOUCH_PACE > 0: the touch loads go out one per lane per round, s_sleep
+// TOUCH_PACE between rounds, and stop once wave 0 holds the exchange's total --
+// a late workgroup (short wait) then has few touches left to drain before its
+// next pass.  0: all issued at once (drained after the exchange).
+constexpr int TOUCH_PACE = GK_RES_TOUCH_PACE;
 
 template <int RW, int LW, int MODE>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
@@ -1740,6 +1784,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     __shared__ double bc[1];
     __shared__ int okf;
     __shared__ double hsh[RHMAX + 1];
+    __shared__ int xdone;  // TOUCH_PACE: the exchange in progress has completed
     const int t = threadIdx.x;
     constexpr int mode = MODE;
     const int j = a.j, np = res_np(mode, j);
@@ -1892,9 +1937,11 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         clk.passed(a.stamps);
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
+        if (TOUCH_PACE > 0 && t == 0) xdone = 0;
         __syncthreads();
         if (t < 64) {
-            res_exchange<WT / 64, false, MODE == RES_MGS>(a, xi, sm, bc, &okf);
+            res_exchange<WT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
+            if (TOUCH_PACE > 0 && t == 0) *(volatile int *)&xdone = 1;
         } else if constexpr (TOUCH > 0) {
             if (touch_col >= 0) {
                 // lines [0, 32*TOUCH) of the workgroup's register-resident part of
@@ -1903,8 +1950,12 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + c0 * WT);
                 const i64 lines = (i64)32 * (cend - c0 < TOUCH ? (cend - c0 > 0 ? cend - c0 : 0) : TOUCH);
                 for (i64 l = t - 64; l < lines; l += WT - 64) {
+                    if constexpr (TOUCH_PACE > 0) {
+                        if (*(volatile int *)&xdone) break;  // wave-uniform: one LDS word
+                    }
                     const char *ptr = base + l * 128;
                     asm volatile("global_load_dword %0, %1, off" : "+v"(touch_sink) : "v"(ptr) : "memory");
+                    if constexpr (TOUCH_PACE > 0) __builtin_amdgcn_s_sleep(TOUCH_PACE);
                 }
             }
         }

@@ -39,6 +39,21 @@ def analyse(pub: np.ndarray, seen: np.ndarray) -> dict:
     # the fastest workgroup's pass after the total was known
     gap = (pub[:, 1:].min(axis=0) - seen[:, :-1].max(axis=0)) * 1e3 if pub.shape[1] > 1 else np.zeros(1)
     pct = lambda v, q: round(float(np.percentile(v, q)), 3)  # noqa: E731
+    # is lateness a property of the workgroup (static imbalance) or of the pass (noise)?
+    late = (pub - np.median(pub, axis=0)[None, :]) * 1e3  # us behind the median publisher
+    wg_late = late.mean(axis=1)
+    h = late.shape[1] // 2
+    persist = float(np.corrcoef(late[:, :h].mean(axis=1), late[:, h:].mean(axis=1))[0, 1]) if h >= 2 else 0.0
+    # does being late at exchange p lengthen the next pass (seen_p -> publish_{p+1})?
+    # (e.g. the L2 touch loads a late workgroup issued during a short wait still draining)
+    follow = {}
+    if pub.shape[1] > 1:
+        nxt = (pub[:, 1:] - seen[:, :-1]) * 1e3
+        lp = late[:, :-1]
+        q90, q50 = np.percentile(lp, 90, axis=0), np.percentile(lp, 50, axis=0)
+        follow = {"late10pct": round(float(nxt[lp >= q90[None, :]].mean()), 3),
+                  "early50pct": round(float(nxt[lp <= q50[None, :]].mean()), 3),
+                  "corr": round(float(np.corrcoef(lp.ravel(), nxt.ravel())[0, 1]), 3)}
     return {"workgroups": G, "exchanges": int(ok.sum()),
             "wait_us": {"mean": round(float(wait.mean()), 3), "p50": pct(wait, 50), "p90": pct(wait, 90)},
             "skew_us": {"mean": round(float(skew.mean()), 3), "p50": pct(skew, 50), "p90": pct(skew, 90),
@@ -47,6 +62,11 @@ def analyse(pub: np.ndarray, seen: np.ndarray) -> dict:
                         "p50": pct(prop, 50), "p90": pct(prop, 90), "max": round(float(prop.max()), 3)},
             "xcd_share_last": [round(float(v), 3) for v in xcd_last],
             "last_wg_most_often": int(np.bincount(who).argmax()),
+            "wg_lateness_us": {"sd_of_wg_means": round(float(wg_late.std()), 3),
+                               "sd_per_exchange": round(float(late.std(axis=0).mean()), 3),
+                               "halves_correlation": round(persist, 3),
+                               "by_xcd": [round(float(wg_late[k::8].mean()), 3) for k in range(min(8, G))]},
+            "next_pass_us_by_lateness": follow,
             "seen_to_next_publish_min_us": round(float(np.median(gap)), 3)}
 
 
