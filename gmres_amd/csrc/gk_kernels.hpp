@@ -1769,12 +1769,18 @@ constexpr bool XPF = XPF_MODE != 0;
 #endif
 constexpr int TOUCH = GK_RES_TOUCH;
 #ifndef GK_RES_TOUCH_PACE
-#define GK_RES_TOUCH_PACE 0
+#define GK_RES_TOUCH_PACE 24
 #endif
-// TOUCH_PACE > 0: the touch loads go out one per lane per round, s_sleep
-// TOUCH_PACE between rounds, and stop once wave 0 holds the exchange's total --
-// a late workgroup (short wait) then has few touches left to drain before its
-// next pass.  0: all issued at once (drained after the exchange).
+// TOUCH_PACE > 0 (MGS-R step launches): the touch loads go out one per lane per
+// round, s_sleep TOUCH_PACE between rounds, and stop once wave 0 holds the
+// exchange's total -- a late workgroup (short wait) then has few touches left to
+// drain before its next pass (the trace: a workgroup late at exchange p ran its
+// next pass 0.5 us longer).  A/B at 4096^2 (profiles/r02/ab_touch_pace.jsonl):
+// MGS-R 41.55 -> 41.28 us per projection at 24 (8: 41.37); the reflection chains
+// run slower with it (pace 8: 41.9 -> 42.7 us), so they keep the all-at-once touch.
+// 0: all issued at once (drained after the exchange).  Interleaving the resident
+// chunks over the grid (chunk b + kG instead of a contiguous range per workgroup)
+// was measured too: 41.5 -> 48.0 us (DRAM row locality lost).
 constexpr int TOUCH_PACE = GK_RES_TOUCH_PACE;
 
 template <int RW, int LW, int MODE>
@@ -1784,9 +1790,10 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     __shared__ double bc[1];
     __shared__ int okf;
     __shared__ double hsh[RHMAX + 1];
-    __shared__ int xdone;  // TOUCH_PACE: the exchange in progress has completed
+    __shared__ int xdone;  // PACE: the exchange in progress has completed
     const int t = threadIdx.x;
     constexpr int mode = MODE;
+    constexpr int PACE = MODE == RES_MGS ? TOUCH_PACE : 0;
     const int j = a.j, np = res_np(mode, j);
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
     const i64 nch = a.nres2 / WT;
@@ -1937,11 +1944,11 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         clk.passed(a.stamps);
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
-        if (TOUCH_PACE > 0 && t == 0) xdone = 0;
+        if (PACE > 0 && t == 0) xdone = 0;
         __syncthreads();
         if (t < 64) {
             res_exchange<WT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
-            if (TOUCH_PACE > 0 && t == 0) *(volatile int *)&xdone = 1;
+            if (PACE > 0 && t == 0) *(volatile int *)&xdone = 1;
         } else if constexpr (TOUCH > 0) {
             if (touch_col >= 0) {
                 // lines [0, 32*TOUCH) of the workgroup's register-resident part of
@@ -1950,12 +1957,12 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + c0 * WT);
                 const i64 lines = (i64)32 * (cend - c0 < TOUCH ? (cend - c0 > 0 ? cend - c0 : 0) : TOUCH);
                 for (i64 l = t - 64; l < lines; l += WT - 64) {
-                    if constexpr (TOUCH_PACE > 0) {
+                    if constexpr (PACE > 0) {
                         if (*(volatile int *)&xdone) break;  // wave-uniform: one LDS word
                     }
                     const char *ptr = base + l * 128;
                     asm volatile("global_load_dword %0, %1, off" : "+v"(touch_sink) : "v"(ptr) : "memory");
-                    if constexpr (TOUCH_PACE > 0) __builtin_amdgcn_s_sleep(TOUCH_PACE);
+                    if constexpr (PACE > 0) __builtin_amdgcn_s_sleep(PACE);
                 }
             }
         }
