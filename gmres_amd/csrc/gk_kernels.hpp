@@ -1761,13 +1761,27 @@ constexpr bool XPF = XPF_MODE != 0;
 // TOUCH chunks (4 KiB each) of the NEXT pass's dot column -- the one that
 // comes from HBM -- into L2 with one dword load per 128-B line into a sink
 // register, so the memory pipe works through the wait.  0 = off; A/B at
-// 4096^2 (profiles/r02/ab_touch*.jsonl): 8 +-0, 16 -1.5 %, 32 -2.2 % per
-// projection (MGS-R 42.4 -> 41.7 us, HH 43.2 -> 42.2 us), 48 / 64 slower
-// (the touched lines outgrow the 128 KiB per-CU share of L2).
+// 4096^2 with one granule array (profiles/r02/ab_touch*.jsonl): 8 +-0, 16 -1.5 %,
+// 32 -2.2 % per projection (MGS-R 42.4 -> 41.7 us, HH 43.2 -> 42.2 us), 48 / 64
+// slower (the touched lines outgrow the 128 KiB per-CU share of L2); the depths
+// now in use are below.
 #ifndef GK_RES_TOUCH
-#define GK_RES_TOUCH 32
+#define GK_RES_TOUCH 24
 #endif
 constexpr int TOUCH = GK_RES_TOUCH;
+#ifndef GK_RES_TOUCH_MGS
+#define GK_RES_TOUCH_MGS 28
+#endif
+// Touched chunks per workgroup: MGS-R launches (paced touches) TOUCH_MGS, the
+// reflection chains (burst) TOUCH.  A/B at 4096^2 after the granule replicas and the
+// pacing (profiles/r02/ab_touch_depth_paced.jsonl, ab_touch_depth_mode.jsonl): MGS-R
+// 16 / 20 / 24 / 28 / 32 / 40 / 48 -> 41.47 / 41.08 / 41.04 / 40.78 / 41.17 / 42.7 / 43.6
+// us per projection (two boxes); Householder 24 vs 32: 40.76 vs 41.96 us per reflection.
+constexpr int TOUCH_MGS = GK_RES_TOUCH_MGS;
+#ifndef GK_RES_ROT
+#define GK_RES_ROT 0
+#endif
+constexpr int RES_ROT = GK_RES_ROT;
 #ifndef GK_RES_TOUCH_PACE
 #define GK_RES_TOUCH_PACE 24
 #endif
@@ -1794,11 +1808,15 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     const int t = threadIdx.x;
     constexpr int mode = MODE;
     constexpr int PACE = MODE == RES_MGS ? TOUCH_PACE : 0;
+    constexpr int TCH = MODE == RES_MGS ? TOUCH_MGS : TOUCH;  // touched chunks per workgroup
     const int j = a.j, np = res_np(mode, j);
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
     const i64 nch = a.nres2 / WT;
-    const i64 c0 = (i64)blockIdx.x * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
-    const i64 l0 = (i64)gridDim.x * a.r2e + (i64)blockIdx.x * a.l2e, lend = l0 + a.l2e < nch ? l0 + a.l2e : nch;
+    // chunk range of this workgroup: that of workgroup (b + ROT) mod G (ROT != 0: an A/B
+    // knob that moves the data relative to the XCDs)
+    const i64 bq = ((i64)blockIdx.x + RES_ROT) % gridDim.x;
+    const i64 c0 = bq * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
+    const i64 l0 = (i64)gridDim.x * a.r2e + bq * a.l2e, lend = l0 + a.l2e < nch ? l0 + a.l2e : nch;
     const i64 tail0 = mode == RES_HH_UP ? a.tail0 : 0;
     const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
     double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
@@ -1949,13 +1967,13 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         if (t < 64) {
             res_exchange<WT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
             if (PACE > 0 && t == 0) *(volatile int *)&xdone = 1;
-        } else if constexpr (TOUCH > 0) {
+        } else if constexpr (TCH > 0) {
             if (touch_col >= 0) {
-                // lines [0, 32*TOUCH) of the workgroup's register-resident part of
+                // lines [0, 32*TCH) of the workgroup's register-resident part of
                 // the column (contiguous from chunk c0); all loads land in one sink
                 // register, drained below before anything can reuse it
                 const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + c0 * WT);
-                const i64 lines = (i64)32 * (cend - c0 < TOUCH ? (cend - c0 > 0 ? cend - c0 : 0) : TOUCH);
+                const i64 lines = (i64)32 * (cend - c0 < TCH ? (cend - c0 > 0 ? cend - c0 : 0) : TCH);
                 for (i64 l = t - 64; l < lines; l += WT - 64) {
                     if constexpr (PACE > 0) {
                         if (*(volatile int *)&xdone) break;  // wave-uniform: one LDS word
@@ -1967,7 +1985,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             }
         }
         __syncthreads();
-        if constexpr (TOUCH > 0) asm volatile("s_waitcnt vmcnt(0)" : : "v"(touch_sink) : "memory");
+        if constexpr (TCH > 0) asm volatile("s_waitcnt vmcnt(0)" : : "v"(touch_sink) : "memory");
         ++xi;
         h = bc[0];
         clk.waited(a.stamps);
