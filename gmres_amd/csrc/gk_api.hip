@@ -614,6 +614,14 @@ constexpr int RES_R2_BIG = 12;          // two register arrays of 12 double2 fit
 #define GK_RES_RW 88
 #endif
 constexpr int RES_RW = GK_RES_RW, RES_LW = 38;  // w-only variant: double2 of w per thread in registers / LDS
+#ifndef GK_RES_RW_HH
+#define GK_RES_RW_HH 90
+#endif
+// The reflection chains hold two chunks more (RW 90 with a 6-deep batch: 90 + 38 chunks =
+// the whole 4096^2 slab on chip, nothing streamed): A/B at 4096^2 (profiles/r02/ab_rw_hh.jsonl)
+// Householder 41.05 -> 40.57 us per reflection, while the MGS-R step keeps 88 / 8 (41.2 vs
+// 41.67 us with 90 / 6).
+constexpr int RES_RW_HH = GK_RES_RW_HH;
 
 struct ResPlan {
     int G = 0, r2 = 0, l2 = 0;
@@ -642,7 +650,7 @@ bool wonly_pays(i64 n2, int G) {
 //   wave 0 kept for the exchange: R2 in {2,4,8}, PF + CW;
 //   else w and the running column in 2 x 12 registers, plus (GK_TUNE_RES_LDS)
 //   w of 18 more chunks per workgroup in LDS, the rest streamed.
-bool res_plan(gk_ctx *c, ResPlan &p) {
+bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
     if (c->tune_res == 0 || c->res_broken || c->m > gk::RHMAX || c->res_cus <= 0 || c->res_gath == nullptr)
         return false;
     if (collective(c) && !(c->xs_on && c->nranks > 1)) return false;
@@ -681,7 +689,7 @@ bool res_plan(gk_ctx *c, ResPlan &p) {
         // w only, one wave per SIMD: 16 B/unknown per projection for ~100 chunks per workgroup
         p.G = gmax;
         p.wo = true;
-        spread(gk::WT, RES_RW, RES_LW);
+        spread(gk::WT, hh ? RES_RW_HH : RES_RW, RES_LW);
         p.lds = RES_LW * gk::WT * (int)sizeof(double2);
         return true;
     } else {
@@ -724,14 +732,16 @@ int launch_res_t(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 
 template <int MODE>
 int launch_wres_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    constexpr int RW = MODE == gk::RES_MGS ? RES_RW : RES_RW_HH;
+    constexpr int WBT = MODE == gk::RES_MGS ? gk::WB : gk::WB_HH;
     static std::atomic<int> attr[ATTR_DEVS];
     if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
     if (attr[c->dev].load() < p.lds) {
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RES_RW, RES_LW, MODE>),
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RW, RES_LW, MODE, WBT>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
         attr[c->dev] = p.lds;
     }
-    gk::k_mgs_wres<RES_RW, RES_LW, MODE><<<p.G, gk::WT, p.lds, c->st>>>(a);
+    gk::k_mgs_wres<RW, RES_LW, MODE, WBT><<<p.G, gk::WT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
 }
@@ -1156,7 +1166,7 @@ int gram(gk_ctx *c, const double *base, int ncols, std::vector<double> &G) {
 int reflect_chain_down(gk_ctx *c, double *v, int k, i64 unit_g = -1, int flags = 0) {
     double *P = c->V;
     ResPlan rp;
-    if (res_plan(c, rp))
+    if (res_plan(c, rp, true))
         return res_step(c, k, rp, nullptr, 0, nullptr, nullptr, gk::RES_HH_DOWN, v, unit_g, flags);
     if (flags != 0) return set_err(GK_ERR_STATE, "resident chain flags without a resident plan");
     int s0 = 0, s1 = 1;
@@ -1855,7 +1865,7 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
     // (GK_TUNE_HH_FUSE): the DOWN chain builds e_j itself (no k_set_unit), the UP
     // chain ends with the fix-up and P(:,j+1) = w/||w|| (no k_hh_fix, no k_scale).
     ResPlan rp;
-    const bool res = res_plan(c, rp);
+    const bool res = res_plan(c, rp, true);
     const bool fuse = res && rp.wo && c->tune_hh_fuse != 0;
     // v_j = e_j ; v_j = P_1 .. P_j e_j
     if (!fuse) {

@@ -1751,6 +1751,10 @@ constexpr int WT = 256;  // threads per workgroup (4 waves, one per SIMD)
 #define GK_RES_XPF 0
 #endif
 constexpr int WB = GK_RES_WB;        // double2 per column per batch in flight per thread
+#ifndef GK_RES_WB_HH
+#define GK_RES_WB_HH 6
+#endif
+constexpr int WB_HH = GK_RES_WB_HH;  // the reflection chains' batch (their RW is larger)
 // XPF 1: every wave loads the next pass's first batch before the exchange wait;
 // 2: waves 1..3 only (wave 0 runs the exchange: its polls would queue behind
 // its own prefetch loads, vmcnt retiring in issue order).  Measured: 1 is
@@ -1797,7 +1801,7 @@ constexpr int RES_ROT = GK_RES_ROT;
 // was measured too: 41.5 -> 48.0 us (DRAM row locality lost).
 constexpr int TOUCH_PACE = GK_RES_TOUCH_PACE;
 
-template <int RW, int LW, int MODE>
+template <int RW, int LW, int MODE, int WBT = WB>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     extern __shared__ double2 lw[];  // [LW][WT]
     __shared__ double sm[WT / 64];
@@ -1855,14 +1859,14 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     // XPF: the first batch of a pass (its two columns are known before the dot
     // that scales it) is loaded before the previous pass's exchange wait, so the
     // memory pipe is busy while the all-gather completes.
-    double2 pa[WB], pb[WB];
+    double2 pa[WBT], pb[WBT];
     const bool xpf_wave = XPF_MODE == 1 || (XPF_MODE == 2 && t >= 64);
     auto load_first = [&](int i, int q, bool dot) {
         if (!xpf_wave) return;
         const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
         const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
 #pragma unroll
-        for (int u = 0; u < WB; ++u) {
+        for (int u = 0; u < WBT; ++u) {
             const i64 c = c0 + u;
             if (u < RW && c < cend) {
                 pa[u] = ldv<true>(A2 + c * WT + t);
@@ -1877,12 +1881,12 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
         const bool dot = kind == RK_DOT;
         double acc = 0.0;
-        // registers: batches of WB chunks, both columns in flight
+        // registers: batches of WBT chunks, both columns in flight
 #pragma unroll
-        for (int k0 = 0; k0 < RW; k0 += WB) {
-            double2 av[WB], bv[WB];
+        for (int k0 = 0; k0 < RW; k0 += WBT) {
+            double2 av[WBT], bv[WBT];
 #pragma unroll
-            for (int u = 0; u < WB; ++u) {
+            for (int u = 0; u < WBT; ++u) {
                 const i64 c = c0 + k0 + u;
                 if (XPF && k0 == 0 && xpf_wave) {
                     av[u] = pa[u];
@@ -1893,7 +1897,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 }
             }
 #pragma unroll
-            for (int u = 0; u < WB; ++u) {
+            for (int u = 0; u < WBT; ++u) {
                 const int k = k0 + u;
                 if (k < RW && c0 + k < cend) {
                     wr[k].x = wr[k].x - ch * av[u].x;
@@ -1903,10 +1907,10 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             }
         }
         // LDS: the same, w from / to LDS
-        for (int k0 = 0; k0 < LW; k0 += WB) {
-            double2 av[WB], bv[WB];
+        for (int k0 = 0; k0 < LW; k0 += WBT) {
+            double2 av[WBT], bv[WBT];
 #pragma unroll
-            for (int u = 0; u < WB; ++u) {
+            for (int u = 0; u < WBT; ++u) {
                 const i64 c = l0 + k0 + u;
                 if (k0 + u < LW && c < lend) {
                     av[u] = ldv<true>(A2 + c * WT + t);
@@ -1914,7 +1918,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 }
             }
 #pragma unroll
-            for (int u = 0; u < WB; ++u) {
+            for (int u = 0; u < WBT; ++u) {
                 const int k = k0 + u;
                 if (k < LW && l0 + k < lend) {
                     double2 wv = lw[k * WT + t];
