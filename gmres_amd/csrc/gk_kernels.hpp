@@ -1800,6 +1800,12 @@ constexpr int RES_ROT = GK_RES_ROT;
 // chunks over the grid (chunk b + kG instead of a contiguous range per workgroup)
 // was measured too: 41.5 -> 48.0 us (DRAM row locality lost).
 constexpr int TOUCH_PACE = GK_RES_TOUCH_PACE;
+#ifndef GK_RES_TOUCH_PACE_HH
+#define GK_RES_TOUCH_PACE_HH 0
+#endif
+// the reflection chains' pacing (0 = burst); re-measured after the depth / residency
+// re-tune (profiles/r02/ab_pace_retune.jsonl): 8 / 24 -> 41.06 / 41.1 vs 40.57 us burst
+constexpr int TOUCH_PACE_HH = GK_RES_TOUCH_PACE_HH;
 
 template <int RW, int LW, int MODE, int WBT = WB>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
@@ -1811,7 +1817,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     __shared__ int xdone;  // PACE: the exchange in progress has completed
     const int t = threadIdx.x;
     constexpr int mode = MODE;
-    constexpr int PACE = MODE == RES_MGS ? TOUCH_PACE : 0;
+    constexpr int PACE = MODE == RES_MGS ? TOUCH_PACE : TOUCH_PACE_HH;
     constexpr int TCH = MODE == RES_MGS ? TOUCH_MGS : TOUCH;  // touched chunks per workgroup
     const int j = a.j, np = res_np(mode, j);
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
