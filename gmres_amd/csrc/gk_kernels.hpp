@@ -1806,15 +1806,6 @@ constexpr int TOUCH_PACE = GK_RES_TOUCH_PACE;
 // the reflection chains' pacing (0 = burst); re-measured after the depth / residency
 // re-tune (profiles/r02/ab_pace_retune.jsonl): 8 / 24 -> 41.06 / 41.1 vs 40.57 us burst
 constexpr int TOUCH_PACE_HH = GK_RES_TOUCH_PACE_HH;
-#ifndef GK_RES_SPAR
-#define GK_RES_SPAR 0
-#endif
-// SPAR (MGS-R launches, even grids): the streamed part of w is owned by workgroup pairs
-// (2q, 2q+1) -- element E = (q + k G/2) WT + t -- the even one taking every fourth k and
-// the odd one the rest, so the even XCDs (which lag by ~0.5-0.8 us per pass, an XCD
-// property: profiles/r02/res_trace_rotation.jsonl) stream a quarter of what the odd
-// ones do.  0: grid-stride ownership (every workgroup the same share).
-constexpr bool RES_SPAR = GK_RES_SPAR != 0;
 
 template <int RW, int LW, int MODE, int WBT = WB>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
@@ -1844,16 +1835,6 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     int touch_sink = 0;
     const i64 sstride = (i64)gridDim.x * WT;
     const i64 sbase = a.nres2 + (i64)blockIdx.x * WT + t;
-    const bool spar = MODE == RES_MGS && RES_SPAR && (gridDim.x & 1) == 0;
-    auto sown = [&](auto &&f) {  // spar: this thread's streamed elements (one each call)
-        const i64 half = gridDim.x >> 1, q = blockIdx.x >> 1, S = n2 - a.nres2;
-        const bool odd = (blockIdx.x & 1) != 0;
-        for (i64 k = 0;; ++k) {
-            const i64 E = (q + k * half) * WT + t;
-            if (E >= S) break;
-            if (((k & 3) == 0) != odd) f(a.nres2 + E);
-        }
-    };
     double2 wr[RW];
     if (mode == RES_HH_DOWN && a.unit_init) {
         // w = e_u built in place (gmres_hh.f90:257-264): no k_set_unit launch, no read
@@ -1954,17 +1935,6 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 }
             }
         }
-        if (spar) {
-            sown([&](i64 e) {
-                double2 wv = W2[e];
-                const double2 av = ldv<true>(A2 + e);
-                const double2 bv = dot ? B2[e] : double2{0.0, 0.0};
-                wv.x = wv.x - ch * av.x;
-                wv.y = wv.y - ch * av.y;
-                W2[e] = wv;
-                red(acc, wv, bv, kind, e, false);
-            });
-        } else {
         for (i64 e0 = sbase; e0 < n2; e0 += 2 * sstride) {  // streamed part: 32 B/unknown
             double2 wv[2], av[2], bv[2];
 #pragma unroll
@@ -1986,7 +1956,6 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                     red(acc, wv[u], bv[u], kind, e, mode == RES_HH_UP && 2 * a.nres2 < tail0);
                 }
             }
-        }
         }
         if ((a.n & 1) && blockIdx.x == 0 && t == 0) {  // odd-length tail element
             const i64 e = a.n - 1;
@@ -2169,14 +2138,9 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             const double2 v = lw[k * WT + t];
             O2[(l0 + k) * WT + t] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
         }
-    auto scale_out = [&](i64 e) {
+    for (i64 e = sbase; e < n2; e += sstride) {
         const double2 v = W2[e];
         O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
-    };
-    if (spar) {
-        sown(scale_out);
-    } else {
-        for (i64 e = sbase; e < n2; e += sstride) scale_out(e);
     }
     if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     clk.finish(a.stamps, mode);
