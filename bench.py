@@ -113,7 +113,10 @@ def cpu_info() -> dict:
     omp = os.environ.get("OMP_NUM_THREADS", "")
     share = min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff
     return {"nproc": os.cpu_count(), "affinity": aff, "OMP_NUM_THREADS": omp or None, "cpu_model": model,
-            "all_cores": share}
+            "omp_threads": share,
+            "omp_threads_note": "the CPU share this process is granted: min(affinity mask, OMP_NUM_THREADS); on "
+                                "the GPU box OMP_NUM_THREADS=16 is the harness's per-GPU CPU share of a larger "
+                                "host, so the sweep stops there (nproc / affinity show the whole machine)"}
 
 
 def _extrapolate(step_t: dict, c0: float, m: int) -> tuple[float, str]:
@@ -134,22 +137,35 @@ def _extrapolate(step_t: dict, c0: float, m: int) -> tuple[float, str]:
     return float(t), f"steps 1..{int(xs[-1]) + 1} timed, step cost fitted a + b j (a={a:.4g} s, b={b:.4g} s)"
 
 
-def cpu_baseline(N: int, m: int, prec: str, degree: int, method: str, cap_all: float, cap_one: float) -> dict:
+def sweep_threads(share: int) -> list[int]:
+    """The reference's strong-scaling pattern (tests/strong_scaling.f90:44-55:
+    1, 2, 4, 8, 16 threads), capped at this process's CPU share, which is
+    always the last point."""
+    ts = [t for t in (1, 2, 4, 8, 16) if t < share]
+    return ts + [share]
+
+
+def cpu_baseline(N: int, m: int, prec: str, degree: int, method: str, cap_full: float, cap_leg: float) -> dict:
     """The reference CPU path timed on this host (rank 0, N = 1 only):
     oracle/_ref/ref_driver = the reference's own gmres_mgsr_omp / gmres_hh_omp
     (kind "reference"); Chebyshev(k) does not exist in the reference, so that
-    config times the restatement (kind "port").  All cores of this process's
-    CPU share (OMP_PROC_BIND=close, OMP_PLACES=cores) for one full cycle when
-    it finishes within cap_all seconds (else a fitted sample), plus 1 core on a
-    bounded sample."""
+    config times the restatement (kind "port").  Thread sweep in the
+    reference's own strong-scaling pattern (1, 2, 4, 8, 16 threads, capped at
+    the process's OpenMP share; OMP_PROC_BIND=close, OMP_PLACES=cores): every
+    leg below the share runs a bounded sample of cycle 1 (the first steps
+    within cap_leg seconds, step cost fitted a + b j and summed over the cycle);
+    the share itself runs one full cycle when it finishes within cap_full
+    seconds (else a fitted sample).  `value` is the fastest leg."""
     from oracle import refrun
 
     info = cpu_info()
     env = {"OMP_PROC_BIND": "close", "OMP_PLACES": "cores"}
-    legs = {}
+    legs = []
     use_ref = refrun.available() and prec in ("identity", "cbpr2")
     solver = ("hh_omp" if prec == "identity" else "hh_prec_omp") if method == "hh" else "mgsr_omp"
-    for name, thr, cap in (("all_cores", info["all_cores"], cap_all), ("one_core", 1, cap_one)):
+    share = info["omp_threads"]
+    for thr in sweep_threads(share):
+        cap = cap_full if thr == share else cap_leg
         t0 = time.perf_counter()
         if use_ref:
             e = dict(env, REF_TIME_CAP=str(cap))
@@ -164,23 +180,25 @@ def cpu_baseline(N: int, m: int, prec: str, degree: int, method: str, cap_all: f
             from oracle import oracle as orc
 
             kind = {"identity": orc.PREC_IDENTITY, "cbpr2": orc.PREC_CBPR2, "cheb": orc.PREC_CHEB}[prec]
-            steps = m if name == "all_cores" else 12
+            steps = m if thr == share else 12
             rr = orc.gmres_mgsr(orc.rhs_ones(N), N, m, prec=kind, degree=degree, variant=orc.MGSR_OMP,
                                 max_cycles=1, step_limit=steps, threads=thr)
             st = {j + 1: float(t) for j, t in enumerate(rr.step_times) if t > 0}
             t_cyc, how = _extrapolate(st, 0.0, m)
             thr_used = thr
-        legs[name] = {"threads": thr_used, "cycle_s": round(t_cyc, 3), "it_s": round(m / t_cyc, 4),
-                      "how": how, "wall_s": round(time.perf_counter() - t0, 1)}
-    a = legs["all_cores"]
-    return {"value": a["it_s"], "unit": "Arnoldi it/s", "cores": a["threads"],
+        legs.append({"threads": thr_used, "cycle_s": round(t_cyc, 3), "it_s": round(m / t_cyc, 4), "how": how,
+                     "wall_s": round(time.perf_counter() - t0, 1)})
+    best = max(legs, key=lambda d: d["it_s"])
+    return {"value": best["it_s"], "unit": "Arnoldi it/s", "cores": best["threads"],
             "kind": "reference" if use_ref else "port",
             "sample": (f"{'oracle/_ref/ref_driver (the reference src/*.f90 built by oracle/Makefile.ref)' if use_ref else 'oracle/gmres_oracle.c (restatement; Chebyshev(k) is not in the reference)'} "
-                       f"{solver} on {N}^2 m={m} prec={prec}, b = A*1, x0 = 0; all cores: {a['how']}; "
-                       f"1 core: {legs['one_core']['how']}"),
-            "one_core": legs["one_core"], "all_cores": a,
+                       f"{solver} on {N}^2 m={m} prec={prec}, b = A*1, x0 = 0; thread sweep "
+                       f"{[d['threads'] for d in legs]} (the reference's strong-scaling pattern, capped at the "
+                       f"process's OpenMP share of {share}); value = the fastest leg ({best['threads']} threads: "
+                       f"{best['how']}); legs below the share: cycle 1 cut after {cap_leg:g} s, a + b j fit"),
+            "sweep": legs,
             "hbm_gbps_alg_as_written": round(cycle_bytes(N * N, m, prec, degree, method, "as_written")
-                                             / a["cycle_s"] / 1e9, 1),
+                                             / best["cycle_s"] / 1e9, 1),
             "host": info, "calibration": "profiles/r02/cpu_calibration.json"}
 
 
@@ -199,6 +217,40 @@ def launch_plan(gpus: int, argv: list[str]) -> dict:
             "env": {"HSA_ENABLE_IPC_MODE_LEGACY": "0"}}
 
 
+def visible_gpus() -> int:
+    """GPUs this process can open, counted WITHOUT the HIP runtime (the
+    launcher touches nothing GPU-side before its ranks start): the KFD topology
+    nodes with a non-zero gpu_id whose DRM render node /dev/dri/renderD<minor>
+    exists and is readable + writable here (a container sees the host's whole
+    topology in sysfs but only its own render nodes), capped by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        nodes = []
+    for d in nodes:
+        try:
+            if int(open(os.path.join(base, d, "gpu_id")).read().strip() or "0") == 0:
+                continue
+            minor = None
+            for line in open(os.path.join(base, d, "properties")):
+                k, _, v = line.partition(" ")
+                if k == "drm_render_minor":
+                    minor = int(v)
+            dev = f"/dev/dri/renderD{minor}" if minor is not None else None
+            if dev is None or os.access(dev, os.R_OK | os.W_OK):
+                n += 1
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def maybe_self_launch(args, argv: list[str]) -> None:
     """N > 1 without a launcher: start one rank per GPU as child processes
     (never exec from a process that may have touched the GPU) and exit with
@@ -212,9 +264,7 @@ def maybe_self_launch(args, argv: list[str]) -> None:
     if args.plan_only:
         print(json.dumps(plan))
         sys.exit(0)
-    import torch
-
-    vis = torch.cuda.device_count()  # counting devices does not initialise them on this image
+    vis = visible_gpus()
     if vis < args.gpus and os.environ.get("GK_BENCH_SAME_DEVICE") != "1":
         print(f"bench.py: --gpus {args.gpus} but only {vis} GPU(s) visible", file=sys.stderr)
         sys.exit(2)
@@ -358,6 +408,77 @@ def diagnostics(ctx, args, run, dist, world: int) -> dict:
                     "all-gather (tools/res_split.py); collective = one partial-slab all-reduce / one halo exchange"}
 
 
+# ------------------------------------------------------- BASELINE configs ---
+GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
+# cycle-1 true residual of each workload from x0 = 0: the reference's own run
+# (tests/golden/reference_runs.json, the reference built from its sources) or,
+# for Chebyshev(8) which the reference does not have, the restatement's
+GOLDEN_OF = {
+    (4096, 95, "identity", "mgsr"): ("reference_runs.json", "mgsr_omp_identity_4096_m95_1cyc_t8"),
+    (1024, 95, "identity", "mgsr"): ("reference_runs.json", "mgsr_omp_identity_1024_m95_3cyc_t8"),
+    (4096, 95, "cheb", "mgsr"): ("oracle_4096.json", "mgsr_cheb8"),
+    (4096, 95, "cbpr2", "mgsr"): ("reference_runs.json", "mgsr_omp_cbpr2_4096_m95_1cyc_t8"),
+    (4096, 95, "identity", "hh"): ("reference_runs.json", "hh_omp_identity_4096_m95_1cyc_t8"),
+}
+# (BASELINE configs[] index, grid, precond, degree, method, timed cycles)
+CONFIG_LEGS = [(1, 1024, "identity", 1, "mgsr", 3), (2, 4096, "cheb", 8, "mgsr", 2), (4, 4096, "identity", 1, "hh", 2)]
+
+
+def cycle1_vs_golden(r1: float, gfile: str | None, gkey: str | None, tol: float = 1e-9) -> dict:
+    if gfile is None:
+        return {"cycle1_true_rel_residual": r1}
+    g = json.load(open(os.path.join(GOLDEN_DIR, gfile)))[gkey]["hist_res"][0]
+    dev = abs(r1 - g) / g
+    return {"cycle1_true_rel_residual": r1, "golden": g, "golden_source": f"tests/golden/{gfile}:{gkey}",
+            "rel_dev": dev, "tol": tol, "pass": bool(dev <= tol)}
+
+
+def config_legs(ga, prof_every: int) -> list[dict]:
+    """After the headline (not part of `value`): short timed legs of the other
+    single-GPU BASELINE configs, each on a fresh context -- a 1-cycle solve from
+    x0 = 0 (warmup; its cycle-1 true residual checked against the golden run),
+    then K timed cycles of a new solve with HIP events on the dominant kernels."""
+    out = []
+    for idx, N, prec, degree, method, K in CONFIG_LEGS:
+        m = 95
+        ns = argparse.Namespace(m=m, method=method, prof_every=prof_every, grid=N, prec=prec, degree=degree)
+        with ga.Context(N, m) as c:
+            c.set_precond(prec, (8.2, 0.2), degree)
+            c.set_rhs_ones()
+
+            def run(k, hist=False):
+                if method == "mgsr":
+                    return ga.gmres_mgsr(c, 1e-15, max_cycles=k, want_verr=False, want_hist=hist)
+                return ga.gmres_hh(c, 1e-15, precondition=prec != "identity", max_cycles=k, want_verr=False,
+                                   want_hist=hist)
+
+            chk = run(1, hist=True)
+            c.profile(1 if method == "hh" else max(1, prof_every))
+            c.profile_reset()
+            c.sync()
+            t0 = time.perf_counter()
+            r = run(K)
+            c.sync()
+            t1 = time.perf_counter()
+            prof = c.profile_read()
+            roof = roofline_entry(prof, ns, c.nloc, r.n_cycles, 1) or {}
+        iters = (r.n_cycles - 1) * m + r.n_out
+        pname = {"identity": "no precond", "cbpr2": "cbpr2", "cheb": f"Chebyshev({degree})"}[prec]
+        leg = {"baseline_config": idx, "workload": f"{N}x{N} Poisson-2D fp64, GMRES-{method.upper()} m={m}, {pname}",
+               "it_s": round(iters / (t1 - t0), 3), "ms_per_cycle": round((t1 - t0) / r.n_cycles * 1e3, 3),
+               "cycles": r.n_cycles,
+               "dominant": {k: roof.get(k) for k in ("kernel", "avg_launch_us", "per_projection_us", "achieved",
+                                                     "frac")},
+               "check": cycle1_vs_golden(chk.hist_res[0], *GOLDEN_OF[(N, m, prec, method)])}
+        if prof.get("prec", (0, 0))[1] > 0:  # the temporal-blocked Chebyshev pass (k_cheb_fused)
+            us = prof["prec"][0] * 1e3 / prof["prec"][1]
+            leg["chebyshev_pass"] = {"avg_launch_us": round(us, 2), "launches_sampled": prof["prec"][1],
+                                     "fused_bytes_per_launch": 24 * N * N,
+                                     "GBps": round(24 * N * N / us / 1e3, 1)}
+        out.append(leg)
+    return out
+
+
 # ------------------------------------------------------------------- main ---
 def main() -> None:
     ap = argparse.ArgumentParser()
@@ -372,7 +493,10 @@ def main() -> None:
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-cap", type=float, default=45.0,
                     help="seconds: all-core reference leg runs a full cycle if it finishes within this, else a sample")
-    ap.add_argument("--cpu-cap-one", type=float, default=15.0, help="seconds of the 1-core sample")
+    ap.add_argument("--cpu-cap-leg", type=float, default=8.0,
+                    help="seconds of cycle 1 sampled per thread-sweep leg below the process's OpenMP share")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="N=1: skip the short timed legs of BASELINE configs 2, 3 and 5 after the headline")
     ap.add_argument("--no-prof", action="store_true", help="no HIP-event kernel timing in the timed region")
     ap.add_argument("--collective", default="auto", choices=["auto", "rccl", "xgmi"],
                     help="N>1: RCCL calls, or the device exchange over xGMI (auto: device exchange if its "
@@ -426,11 +550,11 @@ def main() -> None:
     ctx.set_precond(args.prec, (8.2, 0.2), args.degree)
     ctx.set_rhs_ones()
 
-    def run(cycles: int):
+    def run(cycles: int, hist: bool = False):
         if args.method == "mgsr":
-            return ga.gmres_mgsr(ctx, 1e-15, max_cycles=cycles, want_verr=False)
+            return ga.gmres_mgsr(ctx, 1e-15, max_cycles=cycles, want_verr=False, want_hist=hist)
         return ga.gmres_hh(ctx, 1e-15, precondition=(args.prec != "identity"), max_cycles=cycles,
-                           want_verr=False)
+                           want_verr=False, want_hist=hist)
 
     def barrier():
         ctx.sync()
@@ -438,11 +562,13 @@ def main() -> None:
         if dist is not None:
             dist.barrier()
 
+    warm = {}
+
     def guarded_warmup() -> tuple[bool, str]:
         ok, why = 1, ""
         try:
-            if args.warmup > 0:
-                run(args.warmup)
+            if args.warmup > 0:  # from x0 = 0: its cycle 1 is checked against the reference below
+                warm["res"] = run(args.warmup, hist=True)
         except Exception as e:  # noqa: BLE001 - every rank reports, then all agree below
             why = str(e)
             print(f"rank {rank}: warmup failed: {e}", file=sys.stderr)
@@ -487,16 +613,25 @@ def main() -> None:
     iters = (cycles - 1) * m + res.n_out if cycles > 0 else 0
     diag = None if args.no_diag else diagnostics(ctx, args, run, dist, world)
 
+    roof = roofline_entry(prof, args, ctx.nloc, cycles, world) if rank == 0 else None
+    ctx.close()
+    legs = None
+    if rank == 0 and world == 1 and not args.no_configs and (N, m, args.prec, args.method) == (4096, 95, "identity",
+                                                                                                 "mgsr"):
+        legs = config_legs(ga, args.prof_every)
     if rank == 0:
         n = N * N
         it_s = iters / elapsed
         full = cycles == args.steps and res.n_out == m
         b_fused = cycle_bytes(n, m, args.prec, args.degree, args.method, "fused") * cycles
         b_written = cycle_bytes(n, m, args.prec, args.degree, args.method, "as_written") * cycles
-        roof = roofline_entry(prof, args, ctx.nloc, cycles, world)
         cpu = None
         if not args.no_cpu and world == 1:
-            cpu = cpu_baseline(N, m, args.prec, args.degree, args.method, args.cpu_cap, args.cpu_cap_one)
+            cpu = cpu_baseline(N, m, args.prec, args.degree, args.method, args.cpu_cap, args.cpu_cap_leg)
+        check = {"true_rel_residual_after_timed_cycles": resid}
+        if "res" in warm and len(warm["res"].hist_res) > 0:
+            check.update(cycle1_vs_golden(warm["res"].hist_res[0], *GOLDEN_OF.get((N, m, args.prec, args.method),
+                                                                                 (None, None))))
         prec_name = {"identity": "no precond", "cbpr2": "cbpr2", "cheb": f"Chebyshev({args.degree})"}[args.prec]
         out = {
             "metric": METRIC,
@@ -517,7 +652,7 @@ def main() -> None:
                        "collective": collective, "comm_ranks_seen": comm["nranks"], "comm_kind": comm["kind"],
                        "arnoldi_iters": iters},
             "fallback": fallback,
-            "check": {"true_rel_residual_after_timed_cycles": resid},
+            "check": check,
             "hbm_gbps_fused": round(b_fused / elapsed / 1e9, 1) if full else None,
             "cycle_roofline_frac": round(b_fused / elapsed / 1e9 / HBM_PEAK_GBPS, 4) if full else None,
             "hbm_gbps_alg_as_written": round(b_written / elapsed / 1e9, 1) if full else None,
@@ -525,9 +660,9 @@ def main() -> None:
             "roofline": roof,
             "cpu_baseline": cpu,
             "diagnostics": diag,
+            "configs": legs,
         }
         print(json.dumps(out), flush=True)
-    ctx.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -22,14 +22,18 @@ HEADER = os.path.join(os.path.dirname(PKG), "include", "gmres_hip.h")
 
 GK_OK = 0
 GK_ERR_COMM = -6
+GK_TUNE_PROJ_NT = 0
 GK_TUNE_XCHG_TIMEOUT_MS = 7
 GK_TUNE_RES, GK_TUNE_RES_R2, GK_TUNE_RES_SHARE, GK_TUNE_RES_TIMEOUT_MS = 8, 9, 10, 11
 GK_TUNE_VERR_ORDER = 14
 GK_TUNE_HH_FUSE = 15
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
-GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES = range(7)
-KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res"]
+GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES, GK_KID_PREC = range(8)
+KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res", "prec"]
 COMM_KINDS = {0: None, 1: "rccl", 2: "local-group", 3: "xgmi-device-exchange"}
+# resident-step variants (gk_res_info / gk_res_plan_query)
+RES_VARIANTS = {0: None, 1: "prefetch", 2: "pairs", 3: "pairs+lds", 4: "w-only"}
+RES_INFO_KEYS = ["variant", "G", "r2", "l2", "pf", "cw", "wo", "nt", "r2e", "l2e", "lds", "nres2"]
 
 c_int, c_double, c_ll, c_vp = ctypes.c_int, ctypes.c_double, ctypes.c_longlong, ctypes.c_void_p
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -98,6 +102,8 @@ _SIGS = {
     "gk_profile_res_trace": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, _ip, _ip, _dp]),
     "gk_profile_res_split": (c_int, [c_vp, c_int, c_int, _dp, _dp, _dp, ctypes.POINTER(c_ll)]),
     "gk_set_tuning": (c_int, [c_vp, c_int, c_int]),
+    "gk_res_plan_query": (c_int, [c_ll, c_int, c_int, c_int, c_int, ctypes.POINTER(c_ll)]),
+    "gk_res_info": (c_int, [c_vp, c_int, ctypes.POINTER(c_ll)]),
     "gk_lanczos_bounds": (c_int, [c_vp, c_int, _dp, _dp]),
     "gk_vec_count": (c_int, [c_vp, _ip]),
     "gk_vec_apply": (c_int, [c_vp, c_int, c_int, c_int]),

@@ -111,6 +111,7 @@ struct gk_ctx {
     double p0 = 8.2, p1 = 0.2;
     // decomposition / comm
     int nranks = 1, rank = 0, max_lines = 0;
+    int min_lines = 0;  // smallest slab of any rank (0: not gathered yet; ensure_min_lines)
     ncclComm_t comm = nullptr;
     bool comm_ok = false;
     gk_group *lg = nullptr;  // in-process group (GK local comm), else RCCL
@@ -267,8 +268,13 @@ std::string xs_culprit(int code) {
 // After a host wait: did a device exchange miss its deadline?  The exchange is
 // then retired for the life of the context: sequence numbers may differ
 // between ranks after a failed solve (a pipelined step was already queued), so
-// its granules cannot be trusted again -- collectives go to RCCL / the local
-// group (gk_xchg_enable(1) refuses), and resident steps to the launch path.
+// its granules cannot be trusted again (gk_xchg_enable(1) refuses from now on)
+// and resident steps go to the launch path.  The exchange is NOT switched off
+// here: its error flag stays set, so every later exchange of this rank fails at
+// once (NaN results, GK_ERR_COMM).  To continue, the CALLER switches every rank
+// to RCCL / the local group with gk_xchg_enable(0) -- all ranks together, as
+// bench.py's fallback does; flipping only the rank that saw the miss would
+// desynchronise the ranks' collectives.
 int xs_check(gk_ctx *c) {
     const int code = c->xs_err != nullptr ? __atomic_load_n(c->xs_err, __ATOMIC_ACQUIRE) : 0;
     if (code != 0) {
@@ -414,6 +420,10 @@ int bcast(gk_ctx *c, double *buf, int count, int root) {
 // Chebyshev passes need nl = L (their recompute cone).
 int halo_lines(gk_ctx *c, const double *vec, int nl, double *lo, double *hi) {
     if (!collective(c)) return GK_OK;
+    // a slab thinner than the halo would send lines it does not own (and its
+    // neighbours would need lines from two ranks away)
+    if (c->nranks > 1 && (nl < 1 || nl > c->nlines))
+        return set_err(GK_ERR_ARG, "halo of %d lines from a slab of %d lines (rank %d)", nl, c->nlines, c->rank);
     ProfScope ps(c, GK_KID_COMM);
     const int N = c->N;
     const i64 cnt = (i64)nl * N;
@@ -462,6 +472,8 @@ const double *halo_lo(gk_ctx *c) { return (c->nranks > 1 && c->rank > 0) ? c->hl
 const double *halo_hi(gk_ctx *c) { return (c->nranks > 1 && c->rank < c->nranks - 1) ? c->hhi : nullptr; }
 
 // -------------------------------------------------------------- geometry ---
+bool nt_auto_for(i64 max_nloc);
+
 void set_geometry(gk_ctx *c) {
     const int N = c->N;
     c->vec = (N % 2 == 0) ? 2 : 1;
@@ -487,7 +499,7 @@ void set_geometry(gk_ctx *c) {
     // Krylov columns by non-temporal loads once a vector no longer fits
     // comfortably beside them in the 256 MiB Infinity Cache (measured: -20 %
     // projection time at 4096^2, +6 % at 1024^2 where everything is resident).
-    c->nt_auto = (i64)ml * N * 8 > (i64)48 * 1024 * 1024;
+    c->nt_auto = nt_auto_for((i64)ml * N);
     if (npj < 1) npj = 1;
     c->np_pj = (int)npj;
     // elementwise kernels: also from the largest slab (their partial slabs are all-reduced)
@@ -643,24 +655,16 @@ bool wonly_pays(i64 n2, int G) {
     return 16 * wr + 32 * ws < 8 * pr + 16 * pl + 32 * ps;
 }
 
-// Can step j run as one resident launch, and with which variant?  Needs an
-// in-launch reduction path: single rank, or the device exchange (RCCL and the
-// host-side local group cannot be driven from inside a kernel).
+// The variant a slab of nloc local unknowns runs on (pure: no context, no
+// device; gk_res_plan_query exposes it so the CPU tests pin what every
+// production split selects).
 //   fits in 3 x R2 <= 8 registers (w, running column, prefetched column) with
 //   wave 0 kept for the exchange: R2 in {2,4,8}, PF + CW;
+//   else w only in registers + LDS when the byte model says so (GK_TUNE_RES_WONLY);
 //   else w and the running column in 2 x 12 registers, plus (GK_TUNE_RES_LDS)
 //   w of 18 more chunks per workgroup in LDS, the rest streamed.
-bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
-    if (c->tune_res == 0 || c->res_broken || c->m > gk::RHMAX || c->res_cus <= 0 || c->res_gath == nullptr)
-        return false;
-    if (collective(c) && !(c->xs_on && c->nranks > 1)) return false;
-    // Several resident launches on one device spin on each other's partials, so
-    // their streams must run concurrently -- HIP promises nothing about how
-    // streams map to hardware queues.  Auto mode assumes one context per device.
-    if (c->tune_res < 0 && c->res_share > 1) return false;
-    const int gmax = std::max(1, std::min(gk::RGMAX, c->res_cus / std::max(1, c->res_share)));
-    const i64 n2 = c->nloc / 2;
-    const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : RES_R2_BIG;
+void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bool hh, bool nt, ResPlan &p) {
+    const i64 n2 = nloc / 2;
     const i64 dcw = gk::RT - 64;
     // small vectors: no more workgroups than two chunks each (a cheaper all-gather)
     const int gcw = (int)std::max<i64>(1, std::min<i64>(gmax, (n2 + 2 * dcw - 1) / (2 * dcw)));
@@ -685,23 +689,65 @@ bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
         p.G = gcw;
         p.pf = p.cw = true;
         spread(dcw, p.r2, 0);
-    } else if (c->tune_res_wonly > 0 || (c->tune_res_wonly < 0 && wonly_pays(n2, gmax))) {
+    } else if (tune_wonly > 0 || (tune_wonly < 0 && wonly_pays(n2, gmax))) {
         // w only, one wave per SIMD: 16 B/unknown per projection for ~100 chunks per workgroup
         p.G = gmax;
         p.wo = true;
+        p.r2 = 0;  // (the kernel's register part is RES_RW / RES_RW_HH chunks: r2e)
         spread(gk::WT, hh ? RES_RW_HH : RES_RW, RES_LW);
         p.lds = RES_LW * gk::WT * (int)sizeof(double2);
-        return true;
+        p.nt = true;  // V_i non-temporal, V_q default policy (fixed in the kernel)
+        return;
     } else {
         p.G = gmax;
         p.r2 = RES_R2_BIG;
         const i64 dt = gk::RT, regs = (i64)p.G * RES_R2_BIG * dt;
-        p.l2 = (c->tune_res_lds && n2 / dt * dt > regs) ? RES_L2 : 0;
+        p.l2 = (tune_lds && n2 / dt * dt > regs) ? RES_L2 : 0;
         spread(dt, RES_R2_BIG, p.l2);
     }
     p.lds = std::max<int>(RES_LDS_MIN, p.l2 * (p.cw ? gk::RT - 64 : gk::RT) * (int)sizeof(double2));
-    p.nt = c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto);
+    p.nt = nt;
+}
+
+// Non-temporal Krylov-column loads once a vector of the largest slab no longer
+// fits comfortably beside them in the 256 MiB Infinity Cache (set_geometry).
+bool nt_auto_for(i64 max_nloc) { return max_nloc * 8 > (i64)48 * 1024 * 1024; }
+
+// Can step j run as one resident launch, and with which variant?  Needs an
+// in-launch reduction path: single rank, or the device exchange (RCCL and the
+// host-side local group cannot be driven from inside a kernel).
+bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
+    if (c->tune_res == 0 || c->res_broken || c->m > gk::RHMAX || c->res_cus <= 0 || c->res_gath == nullptr)
+        return false;
+    if (collective(c) && !(c->xs_on && c->nranks > 1)) return false;
+    // Several resident launches on one device spin on each other's partials, so
+    // their streams must run concurrently -- HIP promises nothing about how
+    // streams map to hardware queues.  Auto mode assumes one context per device.
+    if (c->tune_res < 0 && c->res_share > 1) return false;
+    const int gmax = std::max(1, std::min(gk::RGMAX, c->res_cus / std::max(1, c->res_share)));
+    const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : RES_R2_BIG;
+    plan_resident(c->nloc, gmax, cap, c->tune_res_lds, c->tune_res_wonly, hh,
+                  c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p);
     return true;
+}
+
+// gk_res_plan_query / gk_res_info layout
+enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, RPI_R2E, RPI_L2E, RPI_LDS, RPI_NRES2 };
+void plan_info(const ResPlan &p, bool on, long long *info) {
+    for (int k = 0; k < GK_RES_INFO_LEN; ++k) info[k] = 0;
+    if (!on) return;
+    info[RPI_VARIANT] = p.wo ? GK_RES_WONLY : (p.pf ? GK_RES_PREFETCH : (p.l2 > 0 ? GK_RES_PAIRS_LDS : GK_RES_PAIRS));
+    info[RPI_G] = p.G;
+    info[RPI_R2] = p.r2;
+    info[RPI_L2] = p.l2;
+    info[RPI_PF] = p.pf;
+    info[RPI_CW] = p.cw;
+    info[RPI_WO] = p.wo;
+    info[RPI_NT] = p.nt;
+    info[RPI_R2E] = p.r2e;
+    info[RPI_L2E] = p.l2e;
+    info[RPI_LDS] = p.lds;
+    info[RPI_NRES2] = p.nres2;
 }
 
 // hipFuncSetAttribute is per device: remember the dynamic-LDS size set on each.
@@ -913,6 +959,10 @@ dim3 cf_grid(gk_ctx *c, K kern, int L, int &JT) {
         }
         if (jt >= lines) break;
     }
+    // No candidate kept the partial count within a reduction slot (a fixed-JT A/B
+    // build, or gx > NPMAX): grow JT until it does -- a larger grid would write
+    // past its slot into the next one.
+    while (best < 0 && (i64)gx * ((lines + JT - 1) / JT) > gk::NPMAX && JT < lines) JT *= 2;
     return dim3(gx, (lines + JT - 1) / JT, 1);
 }
 
@@ -922,10 +972,12 @@ int launch_cf_acc(gk_ctx *c, int acc, gk::CFArgs &a, i64 *np) {
     dim3 g;
     if (acc == gk::ACC_DOT) {
         g = cf_grid(c, gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_DOT>, L, JT);
+        if ((i64)g.x * g.y > gk::NPMAX) return set_err(GK_ERR_ARG, "Chebyshev pass grid exceeds a reduction slot");
         a.JT = JT;
         gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_DOT><<<g, gk::CF_W, 0, c->st>>>(a);
     } else if (acc == gk::ACC_NORM) {
         g = cf_grid(c, gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NORM>, L, JT);
+        if ((i64)g.x * g.y > gk::NPMAX) return set_err(GK_ERR_ARG, "Chebyshev pass grid exceeds a reduction slot");
         a.JT = JT;
         gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NORM><<<g, gk::CF_W, 0, c->st>>>(a);
     } else {
@@ -956,7 +1008,7 @@ int launch_cf(gk_ctx *c, int L, int acc, gk::CFArgs &a, i64 *np) {
 // sweeps 1..min(k,4) in the first, the rest in the second.
 int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part, const double *c1,
                const double *c2, double theta) {
-    ProfScope ps(c, GK_KID_STENCIL);
+    ProfScope ps(c, GK_KID_PREC);
     const int k = c->pdeg;
     const int g1 = std::min(k, gk::CF_LMAX), g2 = k - g1;
     // On slabs every input of a pass brings L lines of each neighbour (deep halo).
@@ -1014,17 +1066,50 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
     return GK_OK;
 }
 
+// The smallest slab of any rank, gathered once per communicator (collective:
+// every rank reaches it at the same point, the first Chebyshev application):
+// each rank contributes its nlines at its own position of a short vector that
+// is all-reduced by sum.  The decomposition may be any set of consecutive
+// slabs (gk_create / gk_comm_init take any line0, nlines), not only
+// slab_partition's.
+int ensure_min_lines(gk_ctx *c) {
+    if (c->min_lines > 0) return GK_OK;
+    if (!collective(c) || c->nranks == 1) {
+        c->min_lines = c->nlines;
+        return GK_OK;
+    }
+    std::vector<double> v(c->nranks, 0.0);
+    v[c->rank] = c->nlines;
+    double *d = slot(c, 3);
+    HIPCHK(hipMemcpyAsync(d, v.data(), sizeof(double) * c->nranks, hipMemcpyHostToDevice, c->st));
+    CHK(allreduce(c, d, c->nranks, true));
+    HIPCHK(hipMemcpyAsync(v.data(), d, sizeof(double) * c->nranks, hipMemcpyDeviceToHost, c->st));
+    CHK(sync_st(c));
+    int mn = c->nlines;
+    for (double x : v) mn = std::min(mn, (int)x);
+    c->min_lines = mn;
+    return GK_OK;
+}
+
 // Temporal-blocked Chebyshev passes: even N (two points per lane), k <= 8,
-// and on slabs every rank holding at least the first pass's L lines (the deep halo).
-bool cheb_fused_ok(gk_ctx *c) {
-    if (!c->tune_cheb_fused || c->N % 2 != 0 || c->pdeg > 2 * gk::CF_LMAX) return false;
-    if (!collective(c) || c->nranks == 1) return true;
-    return c->N / c->nranks >= std::min(c->pdeg, gk::CF_LMAX);  // the smallest slab of slab_partition
+// and on slabs every rank holding at least the pass's L lines (the deep halo
+// comes from the immediate neighbour only).  The same answer on every rank.
+int cheb_fused_ok(gk_ctx *c, bool *ok) {
+    *ok = false;
+    if (!c->tune_cheb_fused || c->N % 2 != 0 || c->pdeg > 2 * gk::CF_LMAX) return GK_OK;
+    if (!collective(c) || c->nranks == 1) {
+        *ok = true;
+        return GK_OK;
+    }
+    CHK(ensure_min_lines(c));
+    *ok = c->min_lines >= std::min(c->pdeg, gk::CF_LMAX);
+    return GK_OK;
 }
 
 // out = M^-1 z for z already in c->z (cbpr2 or Chebyshev sweeps).
 int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *part) {
-    const bool fused = c->pkind == GK_PREC_CHEB && cheb_fused_ok(c);
+    bool fused = false;
+    if (c->pkind == GK_PREC_CHEB) CHK(cheb_fused_ok(c, &fused));
     if (!fused) CHK(halo(c, c->z));  // the fused passes bring their own deep halos
     if (c->pkind == GK_PREC_CBPR2) {
         // cbpr2 coefficients exactly as chebyshev.f90:19-25
@@ -1320,6 +1405,7 @@ int gk_comm_init(gk_ctx *c, int nranks, int rank, int max_lines, const unsigned 
     c->nranks = nranks;
     c->rank = rank;
     c->max_lines = max_lines;
+    c->min_lines = 0;
     set_geometry(c);
     // A 1-rank RCCL communicator is only built on request (GK_FORCE_RCCL=1): it
     // routes every collective through RCCL on one GPU (used by the tests).
@@ -1355,6 +1441,7 @@ int gk_comm_init_local(gk_ctx *c, gk_group *g, int rank, int max_lines) {
     c->nranks = g->n;
     c->rank = rank;
     c->max_lines = max_lines;
+    c->min_lines = 0;
     set_geometry(c);
     c->lg = g;
     c->res_share = g->n;  // members may share one device: resident launches split its CUs
@@ -1378,6 +1465,7 @@ int gk_comm_init_xgmi(gk_ctx *c, int nranks, int rank, int max_lines) {
     c->nranks = nranks;
     c->rank = rank;
     c->max_lines = max_lines;
+    c->min_lines = 0;
     set_geometry(c);
     return xs_alloc(c);  // comm_ok once gk_xchg_open has mapped the peers
 }
@@ -2218,6 +2306,24 @@ int gk_sync(gk_ctx *c) {
     HIPCHK(hipSetDevice(c->dev));
     CHK(sync_st(c));
     if (c->prof) CHK(prof_harvest(c));
+    return GK_OK;
+}
+
+int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, long long *info) {
+    if (info == nullptr || nloc < 2 || cus < 1 || share < 1) return set_err(GK_ERR_ARG, "bad plan query");
+    const int gmax = std::max(1, std::min(gk::RGMAX, cus / share));
+    ResPlan p;
+    plan_resident(nloc, gmax, RES_R2_BIG, 1, -1, hh != 0, nt < 0 ? nt_auto_for(nloc) : nt != 0, p);
+    plan_info(p, true, info);
+    return GK_OK;
+}
+
+int gk_res_info(gk_ctx *c, int hh, long long *info) {
+    CHK(check_ctx(c));
+    if (info == nullptr) return set_err(GK_ERR_ARG, "null info");
+    ResPlan p;
+    const bool on = res_plan(c, p, hh != 0);
+    plan_info(p, on, info);
     return GK_OK;
 }
 

@@ -712,22 +712,31 @@ struct CFArgs {
 };
 
 // Input prefetch depth: lines t+1 .. t+D are in flight while line t runs
-// through the levels (a D-slot ring; the time loop is unrolled by D so the
-// slots rotate by name -- a register move of an in-flight load would wait for
-// it).  The dot partner of the emitted line rides in the same ring, so no load
-// issued in the current step is waited on before the step ends.
+// through the levels (a D-slot ring).  The time loop is unrolled by CF_U = 6
+// steps, the least common multiple of the 3-line window of d, the 2-line
+// (res, z) pair and the ring, so that every rotation of the per-level state is
+// a renaming of registers instead of v_mov copies (with a 4-step unroll the
+// rotations cost ~60 64-bit moves per step).  The dot partner of the emitted
+// line rides in the same ring, so no load issued in the current step is waited
+// on before the step ends.
 #ifndef GK_CF_DEPTH
-#define GK_CF_DEPTH 0
+#define GK_CF_DEPTH 3
 #endif
-template <bool FIRST>
-constexpr int cf_depth() {
-    return GK_CF_DEPTH > 0 ? GK_CF_DEPTH : (FIRST ? 4 : 3);
-}
+constexpr int CF_U = 6;
+constexpr int CF_D = GK_CF_DEPTH;
+static_assert(CF_U % CF_D == 0, "the ring must rotate a whole number of times per unrolled trip");
 
+// One time step of the level pipeline.  MASK = false: every point of the window
+// and every row any level computes lies inside the grid (or a neighbour's deep
+// halo) -- no per-point selects.  MASK = true (edge windows, the first / last
+// steps of the bottom / top workgroups): rows and points outside the grid are
+// forced to zero at every level, as the per-sweep kernel's boundary does.
+// Both compute every point with the same instructions, so results are
+// identical whichever body a step runs in.
 template <int L, bool FIRST, bool LAST, int ACC>
-__global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
+__global__ __launch_bounds__(CF_W, 2) void k_cheb_fused(CFArgs a) {
     constexpr int H = L + (L & 1);                  // halo, even so a lane's 2 points are kept together
-    constexpr int D = cf_depth<FIRST>();
+    constexpr int D = CF_D;
     const int N = a.N;
     const int lane = threadIdx.x;
     const int keep = CF_PTS - 2 * H;
@@ -735,6 +744,7 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
     const i64 i0 = ob - H + 2 * lane;               // this lane's points i0, i0+1 (i0 even, N even)
     const bool in0 = i0 >= 0 && i0 < N, in1 = i0 + 1 >= 0 && i0 + 1 < N;
     const bool kept = (2 * lane >= H) && (2 * lane < CF_PTS - H) && i0 < N;
+    const bool interior = ob - H >= 0 && ob - H + CF_PTS <= N;  // uniform: no lane outside the grid
     const int j0 = blockIdx.y * a.JT;
     const int j1 = min(j0 + a.JT, a.nlines);
     double acc = 0.0;
@@ -783,92 +793,148 @@ __global__ __launch_bounds__(CF_W) void k_cheb_fused(CFArgs a) {
                 pv[s] = *reinterpret_cast<const double2 *>(a.vdot + (i64)(row - L) * N + i0);
         }
     };
+    // FAST steps: the ring refills from rows inside the slab, so no row / halo /
+    // lane tests; the dot partner row (t + D - L) lies in the grid then too and
+    // is loaded for every lane (only kept rows of [j0, j1) use it).
+    auto issue_fast = [&](int row, int s) {
+        const double2 t = *reinterpret_cast<const double2 *>(a.din + (i64)row * N + i0);
+        pd[s][0] = t.x;
+        pd[s][1] = t.y;
+        if (LAST && ACC == ACC_DOT) pv[s] = *reinterpret_cast<const double2 *>(a.vdot + (i64)(row - L) * N + i0);
+    };
     const int tb0 = j0 - L - 1, tend = j1 + L;
+    auto step = [&](auto maskc, int t, int s) {
+        constexpr bool MASK = decltype(maskc)::value;
+        // emission of "level -1": the input line t (slot s), then slot s
+        // refills with line t + D
+        double ed[2], er[2], ez[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            ed[k] = pd[s][k];
+            er[k] = FIRST ? 0.0 : pr[s][k];
+            ez[k] = FIRST ? 0.0 : pz[s][k];
+        }
+        double2 vd = double2{0.0, 0.0};
+        if (LAST && ACC == ACC_DOT) vd = pv[s];
+        if (MASK || !FIRST) {
+            if (t + D < tend) issue(t + D, s);
+        } else {
+            issue_fast(t + D, s);
+        }
+        if (FIRST) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const double raw = ed[k];
+                ed[k] = raw / a.theta;
+                er[k] = raw;
+                ez[k] = ed[k];
+            }
+        }
+        int row = t;  // row of the current emission
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+            // push the emission into level l
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                dw[l][0][k] = dw[l][1][k];
+                dw[l][1][k] = dw[l][2][k];
+                dw[l][2][k] = ed[k];
+                rm[l][k] = rn[l][k];
+                zm[l][k] = zn[l][k];
+                rn[l][k] = er[k];
+                zn[l][k] = ez[k];
+            }
+            // compute the middle line row-1
+            const int mrow = row - 1;
+            const double left = __shfl_up(dw[l][1][1], 1, 64);
+            const double right = __shfl_down(dw[l][1][0], 1, 64);
+            // (MASK) a row outside the GRID is zero at every level (rows in a
+            // neighbour's halo are real; the deepest ones are wrong but never
+            // reach the kept rows -- the usual L-row recompute cone)
+            const bool rowok = !MASK || ((has_lo || mrow >= 0) && (has_hi || mrow < a.nlines));
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const double W = (k == 0) ? left : dw[l][1][0];
+                const double E = (k == 1) ? right : dw[l][1][1];
+                const double s2 = ((W + E) + dw[l][2][k]) + dw[l][0][k];
+                const double ad = 4.0 * dw[l][1][k] - 1.0 * s2;
+                const double res = rm[l][k] - ad;
+                const double dn = a.c1[l] * dw[l][1][k] + a.c2[l] * res;
+                const double z = zm[l][k] + dn;
+                if constexpr (MASK) {
+                    const bool ok = rowok && (k == 0 ? in0 : in1);
+                    ed[k] = ok ? dn : 0.0;
+                    er[k] = ok ? res : 0.0;
+                    ez[k] = ok ? z : 0.0;
+                } else {
+                    ed[k] = dn;
+                    er[k] = res;
+                    ez[k] = z;
+                }
+            }
+            row = mrow;
+        }
+        // the last level emitted line `row`
+        if (row >= j0 && row < j1 && kept) {
+            const i64 idx = (i64)row * N + i0;
+            if (LAST) {
+                *reinterpret_cast<double2 *>(a.out + idx) = double2{ez[0], ez[1]};
+                if (ACC == ACC_DOT) {
+                    acc = acc + ez[0] * vd.x;
+                    acc = acc + ez[1] * vd.y;
+                } else if (ACC == ACC_NORM) {
+                    acc = acc + ez[0] * ez[0];
+                    acc = acc + ez[1] * ez[1];
+                }
+            } else {
+                *reinterpret_cast<double2 *>(a.dout + idx) = double2{ed[0], ed[1]};
+                *reinterpret_cast<double2 *>(a.rout + idx) = double2{er[0], er[1]};
+                *reinterpret_cast<double2 *>(a.zout + idx) = double2{ez[0], ez[1]};
+            }
+        }
+        // Keep the scheduler from interleaving consecutive steps: across a step
+        // boundary only 4 doubles per point and level are live (d of the two
+        // newest lines, res and z of the newest), and hoisting the next step's
+        // work over the boundary pushes the wave past 256 registers (spills)
+        __builtin_amdgcn_sched_barrier(0);
+    };
     if (j0 < a.nlines) {
 #pragma unroll
         for (int s = 0; s < D; ++s)
             if (tb0 + s < tend) issue(tb0 + s, s);
-        for (int tb = tb0; tb < tend; tb += D) {
+        // Steps [ts0, ts1) compute no row outside the grid at any level: level l
+        // computes row t - l - 1, so rows >= 0 need t >= L and rows < nlines
+        // need t <= nlines (without the neighbour's halo on that side).  A FAST
+        // trip also refills the ring from slab rows only: t + D in [0, nlines).
+        // The trips run as three loops -- masked prologue [tb0, tf0), FAST
+        // [tf0, tf1), masked epilogue [tf1, tend) -- with every boundary a whole
+        // number of CF_U-step trips from tb0 (the ring slots stay compile-time).
+        // Separate loops, not a branch per trip: with both bodies behind one
+        // branch the compiler hoists their common arithmetic above it and spills.
+        const int ts0 = max(has_lo ? tb0 : L, -D), ts1 = min(has_hi ? tend : a.nlines + 1, a.nlines - D);
+        int tf0 = tend, tf1 = tend;
+        if (interior) {
+            const int lo = max(ts0, tb0), hi = min(ts1, tend);
+            const int f0 = tb0 + (lo - tb0 + CF_U - 1) / CF_U * CF_U;
+            const int nf = hi > f0 ? (hi - f0) / CF_U : 0;
+            if (nf > 0) {
+                tf0 = f0;
+                tf1 = f0 + nf * CF_U;
+            }
+        }
+#pragma nounroll
+        for (int seg = 0; seg < 3; ++seg) {
+            if (seg == 1) {
+                for (int tb = tf0; tb < tf1; tb += CF_U) {
 #pragma unroll
-            for (int s = 0; s < D; ++s) {
-                const int t = tb + s;
-                if (t >= tend) break;
-                // emission of "level -1": the input line t (slot s), then slot s
-                // refills with line t + D
-                double ed[2], er[2], ez[2];
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    ed[k] = pd[s][k];
-                    er[k] = FIRST ? 0.0 : pr[s][k];
-                    ez[k] = FIRST ? 0.0 : pz[s][k];
+                    for (int u = 0; u < CF_U; ++u) step(std::false_type{}, tb + u, u % D);
                 }
-                double2 vd = double2{0.0, 0.0};
-                if (LAST && ACC == ACC_DOT) vd = pv[s];
-                if (t + D < tend) issue(t + D, s);
-                if (FIRST) {
+            } else {
+                const int ta = seg == 0 ? tb0 : tf1, tz = seg == 0 ? tf0 : tend;
+                for (int tb = ta; tb < tz; tb += CF_U) {
 #pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        const double raw = ed[k];
-                        ed[k] = raw / a.theta;
-                        er[k] = raw;
-                        ez[k] = ed[k];
-                    }
-                }
-                int row = t;  // row of the current emission
-#pragma unroll
-                for (int l = 0; l < L; ++l) {
-                    // push the emission into level l
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        dw[l][0][k] = dw[l][1][k];
-                        dw[l][1][k] = dw[l][2][k];
-                        dw[l][2][k] = ed[k];
-                        rm[l][k] = rn[l][k];
-                        zm[l][k] = zn[l][k];
-                        rn[l][k] = er[k];
-                        zn[l][k] = ez[k];
-                    }
-                    // compute the middle line row-1
-                    const int mrow = row - 1;
-                    double left = __shfl_up(dw[l][1][1], 1, 64);
-                    double right = __shfl_down(dw[l][1][0], 1, 64);
-                    // a row outside the GRID is zero at every level (rows in a
-                    // neighbour's halo are real; the deepest ones are wrong but
-                    // never reach the kept rows -- the usual L-row recompute cone)
-                    const bool rowok = (has_lo || mrow >= 0) && (has_hi || mrow < a.nlines);
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        const double W = (k == 0) ? left : dw[l][1][0];
-                        const double E = (k == 1) ? right : dw[l][1][1];
-                        const double s2 = ((W + E) + dw[l][2][k]) + dw[l][0][k];
-                        const double ad = 4.0 * dw[l][1][k] - 1.0 * s2;
-                        const double res = rm[l][k] - ad;
-                        const double dn = a.c1[l] * dw[l][1][k] + a.c2[l] * res;
-                        const double z = zm[l][k] + dn;
-                        const bool ok = rowok && (k == 0 ? in0 : in1);
-                        ed[k] = ok ? dn : 0.0;
-                        er[k] = ok ? res : 0.0;
-                        ez[k] = ok ? z : 0.0;
-                    }
-                    row = mrow;
-                }
-                // the last level emitted line `row`
-                if (row >= j0 && row < j1 && kept) {
-                    const i64 idx = (i64)row * N + i0;
-                    if (LAST) {
-                        *reinterpret_cast<double2 *>(a.out + idx) = double2{ez[0], ez[1]};
-                        if (ACC == ACC_DOT) {
-                            acc = acc + ez[0] * vd.x;
-                            acc = acc + ez[1] * vd.y;
-                        } else if (ACC == ACC_NORM) {
-                            acc = acc + ez[0] * ez[0];
-                            acc = acc + ez[1] * ez[1];
-                        }
-                    } else {
-                        *reinterpret_cast<double2 *>(a.dout + idx) = double2{ed[0], ed[1]};
-                        *reinterpret_cast<double2 *>(a.rout + idx) = double2{er[0], er[1]};
-                        *reinterpret_cast<double2 *>(a.zout + idx) = double2{ez[0], ez[1]};
-                    }
+                    for (int u = 0; u < CF_U; ++u)
+                        if (tb + u < tz) step(std::true_type{}, tb + u, u % D);
                 }
             }
         }
@@ -911,21 +977,28 @@ __device__ __forceinline__ void xs_put(u64 *q, unsigned seq, unsigned data) {
     __hip_atomic_store(q, ((u64)seq << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Spin until the granule at q carries `seq`; false once the deadline passed.
-__device__ __forceinline__ bool xs_get(const u64 *q, unsigned seq, u64 deadline, unsigned *data) {
-    for (;;) {
+__device__ __forceinline__ int xs_flag(const int *err) {
+    return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Spin until the granule at q carries `seq`: XG_OK; XG_LATE once the deadline
+// passed (the caller names the straggler); XG_ABORT when another wait of this
+// rank already failed (the sticky flag *err is set, checked every 32 unanswered
+// polls): the exchange is dead, so a doomed launch ends within microseconds
+// instead of waiting out its own deadline, and the first failure stays the one
+// reported.
+enum { XG_ABORT = -1, XG_LATE = 0, XG_OK = 1 };
+__device__ __forceinline__ int xs_get(const u64 *q, unsigned seq, u64 deadline, unsigned *data, const int *err) {
+    for (unsigned it = 1;; ++it) {
         const u64 g = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if ((unsigned)(g >> 32) == seq) {
             *data = (unsigned)g;
-            return true;
+            return XG_OK;
         }
-        if (wall_clock64() > deadline) return false;
+        if (wall_clock64() > deadline) return XG_LATE;
+        if ((it & 31u) == 0 && xs_flag(err) != 0) return XG_ABORT;
         __builtin_amdgcn_s_sleep(2);
     }
-}
-
-__device__ __forceinline__ int xs_flag(const int *err) {
-    return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Which wait missed its deadline (straggler diagnostic, decoded by the host
@@ -977,9 +1050,10 @@ __global__ __launch_bounds__(TPB) void k_xchg(double *__restrict__ buf, int coun
         for (int t = threadIdx.x; t < tot && ok; t += TPB) {
             const int half = t & 1, k = (t >> 1) % plen, src = (t >> 1) / plen;
             unsigned d = 0;
-            ok = xs_get(mine + (((i64)par * XS_MAXR + src) * XS_MAXV + k) * 2 + half, seq, deadline, &d);
+            const int g = xs_get(mine + (((i64)par * XS_MAXR + src) * XS_MAXV + k) * 2 + half, seq, deadline, &d, err);
+            ok = g == XG_OK;
             rv[(src * XS_MAXV + k) * 2 + half] = d;
-            if (!ok) xs_fail(err, MODE == XS_BCAST ? XSE_BCAST : XSE_XCHG, src);
+            if (g == XG_LATE) xs_fail(err, MODE == XS_BCAST ? XSE_BCAST : XSE_XCHG, src);
         }
         if (!ok) bad = 1;
     }
@@ -1049,9 +1123,11 @@ __global__ __launch_bounds__(TPB) void k_xhalo(const double *__restrict__ vec, i
         const u64 *q = slot(mine, side);
         unsigned a = 0, b = 0;
         double v = __builtin_nan("");
-        if (xs_get(q, seq, deadline, &a) && xs_get(q + 1, seq, deadline, &b))
+        int g = xs_get(q, seq, deadline, &a, err);
+        if (g == XG_OK) g = xs_get(q + 1, seq, deadline, &b, err);
+        if (g == XG_OK)
             v = __longlong_as_double((long long)(((u64)b << 32) | a));
-        else
+        else if (g == XG_LATE)
             xs_fail(err, XSE_HALO, side == 0 ? rank - 1 : rank + 1);
         (side == 0 ? hlo : hhi)[e] = v;
     }
@@ -1430,9 +1506,10 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
         bool ok2 = true;
         if (lane < 2 * a.nranks) {
             const int src = lane >> 1, half = lane & 1, r = (int)(blockIdx.x % RES_NREP);
-            ok2 = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV + XS_REP_STEP * r) * 2 + half, seq,
-                         wall_clock64() + a.timeout, &d);
-            if (!ok2) xs_fail(a.err, XSE_RES_RANK, src);
+            const int g = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV + XS_REP_STEP * r) * 2 + half,
+                                 seq, wall_clock64() + a.timeout, &d, a.err);
+            ok2 = g == XG_OK;
+            if (g == XG_LATE) xs_fail(a.err, XSE_RES_RANK, src);
         }
         all_ok = __all(ok2);
         double r = 0.0;

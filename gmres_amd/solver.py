@@ -309,12 +309,33 @@ class Context:
         t0 = t[t > 0].min() if np.any(t > 0) else 0.0
         return (t[:, :, 0] - t0) / tpm.value, (t[:, :, 1] - t0) / tpm.value
 
+    def res_info(self, hh: bool = False) -> dict:
+        """The resident-step plan this context uses now (gk_res_info): variant
+        name (None = launch per projection), workgroups, chunk split."""
+        return _res_dict(lambda buf: nat.hip().gk_res_info(self._h, int(hh), buf), "gk_res_info")
+
     def tune(self, key: int, value: int) -> None:
         """Launch-policy knob (include/gmres_hip.h GK_TUNE_*)."""
         nat.check(nat.hip().gk_set_tuning(self._h, int(key), int(value)), "gk_set_tuning")
 
     def sync(self) -> None:
         nat.check(nat.hip().gk_sync(self._h), "gk_sync")
+
+
+def _res_dict(call, what: str) -> dict:
+    buf = (nat.c_ll * len(nat.RES_INFO_KEYS))()
+    nat.check(call(buf), what)
+    d = dict(zip(nat.RES_INFO_KEYS, (int(v) for v in buf)))
+    d["variant"] = nat.RES_VARIANTS[d["variant"]]
+    return d
+
+
+def res_plan_query(nloc: int, cus: int = 256, share: int = 1, hh: bool = False, nt: int = -1) -> dict:
+    """The resident-step variant a slab of nloc local unknowns selects on a
+    device of `cus` compute units shared by `share` contexts
+    (gk_res_plan_query: host-only, no GPU touched)."""
+    return _res_dict(lambda buf: nat.hip().gk_res_plan_query(int(nloc), int(cus), int(share), int(hh), int(nt), buf),
+                     "gk_res_plan_query")
 
 
 def _alloc_hist(m: int, max_cycles: int, want_hist: bool):

@@ -53,7 +53,8 @@ extern "C" {
 #define GK_KID_COMM 4    /* all-reduce / halo / broadcast (RCCL or device exchange) */
 #define GK_KID_OTHER 5
 #define GK_KID_RES 6     /* resident MGS-R step: whole cascade + norm + scale in one launch */
-#define GK_NKID 7
+#define GK_KID_PREC 7    /* temporal-blocked Chebyshev(k) passes (k_cheb_fused) */
+#define GK_NKID 8
 
 typedef struct gk_ctx gk_ctx;
 typedef struct gk_group gk_group;
@@ -96,7 +97,12 @@ int gk_comm_init_local(gk_ctx *ctx, gk_group *g, int rank, int max_lines);
  *                       a deadline; GK_ERR_COMM if any granule is missing or
  *                       wrong.  Also usable after gk_comm_init (RCCL present):
  *                       a failed test leaves the exchange disabled.
- * Usable together with gk_comm_init (then RCCL remains the fallback). */
+ * Usable together with gk_comm_init (then RCCL remains the fallback).
+ * A missed deadline during a solve (GK_ERR_COMM, naming the late rank or
+ * workgroup) retires the exchange of that context: its later exchanges fail at
+ * once and gk_xchg_enable(1) refuses.  It does NOT switch back to RCCL by
+ * itself -- the caller does, on EVERY rank together, with gk_xchg_enable(0)
+ * (switching only the rank that saw the miss would desynchronise the ranks). */
 int gk_comm_init_xgmi(gk_ctx *ctx, int nranks, int rank, int max_lines);
 int gk_xchg_handle(gk_ctx *ctx, unsigned char handle[64]);
 int gk_xchg_open(gk_ctx *ctx, const unsigned char *handles);
@@ -245,6 +251,35 @@ int gk_profile_res_wg(gk_ctx *ctx, int which, double *pass_ms, double *wait_ms, 
 int gk_profile_res_trace(gk_ctx *ctx, int arm, int j, int mode, unsigned long long *out, int maxwg, int maxx,
                          int *nwg, int *nx, double *tick_per_ms);
 int gk_sync(gk_ctx *ctx);
+
+/* ------------------------------------------- resident-step variant plan ---- */
+/* Which resident kernel an Arnoldi step (and a Householder chain) runs on.
+ * Selection is by the slab's local length and the workgroups available
+ * (compute units / contexts sharing the device), so a 2- / 4- / 8-GPU split
+ * of one grid selects a different variant than the single-GPU run does:
+ *   GK_RES_NONE       no resident launch (one launch per projection);
+ *   GK_RES_PREFETCH   k_mgs_res<R2 in 2,4,8, PF, control wave>: small slabs;
+ *   GK_RES_PAIRS      k_mgs_res<12, 0>: w and the running column in registers;
+ *   GK_RES_PAIRS_LDS  k_mgs_res<12, 18>: the same plus w of 18 chunks per
+ *                     workgroup in LDS, the rest streamed;
+ *   GK_RES_WONLY      k_mgs_wres: w only, in registers + LDS (large slabs).
+ * info[GK_RES_INFO_LEN]: variant, workgroups G, R2, L2, prefetch, control
+ * wave, w-only, non-temporal column loads, register / LDS chunks per
+ * workgroup in use, dynamic LDS bytes, resident double2 of the slab.
+ * gk_res_plan_query: pure host computation for a slab of nloc unknowns on a
+ * device with `cus` compute units shared by `share` contexts; hh != 0 the
+ * reflection chains' plan; nt: -1 auto (from nloc), 0 / 1 forced.  No device
+ * is touched (the CPU tests pin every production split with it).
+ * gk_res_info: the plan this context uses now (its tuning, communicator and
+ * sharing applied); variant GK_RES_NONE when steps run launch by launch. */
+#define GK_RES_NONE 0
+#define GK_RES_PREFETCH 1
+#define GK_RES_PAIRS 2
+#define GK_RES_PAIRS_LDS 3
+#define GK_RES_WONLY 4
+#define GK_RES_INFO_LEN 12
+int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, long long *info);
+int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 
 /* Launch-policy knobs (defaults are the tuned values; for A/B measurement).
  *   GK_TUNE_PROJ_NT        1: non-temporal loads of the Krylov columns in the

@@ -1,0 +1,94 @@
+"""Config 4 (8192^2, m = 95, MGS-R, 8 row-block ranks) on ONE GPU: one
+restart cycle of a single-context 8192^2 run, then the same cycle as 8 slab
+contexts joined by one of the two multi-rank transports:
+
+  local  the in-process communicator (RCCL's message pattern: host barrier +
+         device copies and sums; tests/test_gpu_configs.py runs it in-process)
+  xchg   the device exchange (gk_xchg_local: tagged granules in every peer's
+         receive region, k_xchg / k_xhalo spin-waiting on the device -- the
+         transport of the 8-GPU bench).  Eight contexts of one process then
+         spin on each other's granules from eight streams, which must run
+         concurrently: test_gpu_configs.py starts this module as a child
+         process with GPU_MAX_HW_QUEUES=16 (HIP's default of 4 hardware
+         queues would serialise streams that share a queue).
+
+Prints one JSON line: the single run's and rank 0's residual / final_err,
+whether every rank took identical decisions, and the largest deviations.
+  python tests/config4_run.py local|xchg
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import threading
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+N, M, R = 8192, 95, 8
+
+
+def run(transport: str) -> dict:
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+
+    with ga.Context(N, M) as c:
+        c.set_rhs_ones()
+        ref = ga.gmres_mgsr(c, 1e-15, max_cycles=1, want_verr=False, want_hist=True)
+        xref = c.get_x()
+    parts = ga.slab_partition(N, R)
+    g = ga.LocalGroup(R)
+    ctxs = [ga.Context(N, M, device=0, line0=l0, nlines=nl) for l0, nl in parts]
+    out, err = [None] * R, []
+    try:
+        ml = max(nl for _, nl in parts)
+        for r, c in enumerate(ctxs):
+            c.comm_init_local(g, r, ml)
+        if transport == "xchg":
+            for c in ctxs:
+                c.xchg_local()
+                c.tune(nat.GK_TUNE_XCHG_TIMEOUT_MS, 20000)
+        kinds = {c.comm_info()["kind"] for c in ctxs}
+        plans = {c.res_info()["variant"] for c in ctxs}
+
+        def work(r):
+            try:
+                ctxs[r].set_rhs_ones()
+                ctxs[r].profile(True)
+                ctxs[r].profile_reset()
+                out[r] = (ga.gmres_mgsr(ctxs[r], 1e-15, max_cycles=1, want_verr=False, want_hist=True),
+                          ctxs[r].profile_read())
+            except Exception as e:  # reported below
+                err.append(repr(e))
+
+        th = [threading.Thread(target=work, args=(r,)) for r in range(R)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=300)
+        if err or any(o is None for o in out):
+            return {"ok": False, "error": err or "a rank did not finish"}
+        res = [o[0] for o in out]
+        x = np.concatenate([o.x for o in res])
+        return {
+            "ok": True, "transport": transport, "comm_kinds": sorted(map(str, kinds)), "res_variants": sorted(map(str, plans)),
+            "comm_launches": int(min(o[1]["comm"][1] for o in out)),
+            "same_decisions": len({(o.n_out, o.cycles_out, o.n_cycles) for o in res}) == 1
+            and all(np.array_equal(o.hist_res, res[0].hist_res) for o in res)
+            and all(np.array_equal(o.final_err, res[0].final_err) for o in res),
+            "n_out": res[0].n_out, "hist_res0": float(res[0].hist_res[0]), "ref_hist_res0": float(ref.hist_res[0]),
+            "final_err_max_rel": float(np.max(np.abs(res[0].final_err[:M] - ref.final_err[:M]) / ref.final_err[:M])),
+            "x_max_dev": float(np.max(np.abs(x - xref) / (1e-12 + 1e-9 * np.abs(xref)))),
+        }
+    finally:
+        for c in ctxs:
+            c.close()
+        g.close()
+
+
+if __name__ == "__main__":
+    print(json.dumps(run(sys.argv[1] if len(sys.argv) > 1 else "local")), flush=True)

@@ -92,5 +92,42 @@ def test_cpu_extrapolation_recovers_a_linear_step_cost():
 
 def test_cpu_info_fields():
     info = bench.cpu_info()
-    assert info["nproc"] >= 1 and 1 <= info["all_cores"] <= info["affinity"]
+    assert info["nproc"] >= 1 and 1 <= info["omp_threads"] <= info["affinity"]
+    assert "all_cores" not in info  # the share is the process's OpenMP share, not the machine
     assert isinstance(info["cpu_model"], str)
+
+
+def test_thread_sweep_is_the_reference_pattern():
+    """tests/strong_scaling.f90:44-55 of the reference: 1, 2, 4, 8, 16 threads,
+    here capped at the process's OpenMP share (always the last leg)."""
+    assert bench.sweep_threads(16) == [1, 2, 4, 8, 16]
+    assert bench.sweep_threads(8) == [1, 2, 4, 8]
+    assert bench.sweep_threads(6) == [1, 2, 4, 6]
+    assert bench.sweep_threads(1) == [1]
+    assert bench.sweep_threads(64) == [1, 2, 4, 8, 16, 64]
+
+
+def test_launcher_never_touches_hip():
+    """The self-launching parent counts GPUs from the KFD topology / render
+    nodes and never imports torch or loads the HIP runtime before its ranks
+    start (a HIP call in the launcher would initialise the runtime there)."""
+    code = ("import sys; sys.argv=['bench.py']; import bench; n = bench.visible_gpus(); "
+            "maps = open('/proc/self/maps').read(); "
+            "print(n, 'libamdhip64' in maps, any(k == 'torch' or k.startswith('torch.') for k in sys.modules))")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=_env(), cwd=ROOT,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    n, hip, torch_loaded = out.stdout.split()
+    assert int(n) >= 0 and hip == "False" and torch_loaded == "False"
+    # the refusal path (no GPU here) and --plan-only never import torch either
+    for extra in (["--no-cpu"], ["--plan-only"]):
+        p = subprocess.run([sys.executable, "-X", "importtime", os.path.join(ROOT, "bench.py"), "--gpus", "2", *extra],
+                           capture_output=True, text=True, env=_env(), timeout=120)
+        imported = [ln.rsplit("|", 1)[-1].strip() for ln in p.stderr.splitlines() if ln.startswith("import time:")]
+        assert not any(x == "torch" or x.startswith("torch.") for x in imported), extra
+    assert bench.visible_gpus() == 0 or os.path.exists("/dev/kfd")
+
+
+def test_visible_gpus_respects_visibility_env(monkeypatch):
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.visible_gpus() == 0

@@ -57,10 +57,9 @@ PREC_CASES = [("cbpr2", 1), ("identity", 1)] + [("cheb", k) for k in range(1, 9)
 @pytest.mark.parametrize("N", [16, 64, 129, 130, 256])
 @pytest.mark.parametrize("kind,degree", PREC_CASES)
 def test_precond_bitexact(oracle, N, kind, degree):
-    """Every Chebyshev degree 1..8: one temporal-blocked pass of L = k levels
-    (k <= 4) or two passes (4 + k-4) when N is even; 130 and 256 have more
-    than one 64-line tile (ragged last tile at 130); odd N takes the per-sweep
-    kernels."""
+    """Every Chebyshev degree 1..8: ONE temporal-blocked pass of L = k levels
+    (k <= CF_LMAX = 8) when N is even; 130 and 256 have more than one line tile
+    (ragged last tile at 130); odd N takes the per-sweep kernels."""
     import gmres_amd.solver as S
 
     rng = np.random.default_rng(N + degree)

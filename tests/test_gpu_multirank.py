@@ -148,10 +148,11 @@ def test_rccl_one_rank_communicator(monkeypatch, method, prec):
 @pytest.mark.parametrize("N,nranks", [(66, 3), (20, 4), (16, 5), (130, 2)])
 @pytest.mark.parametrize("degree", [1, 3, 4, 6, 8])
 def test_chebyshev_on_slabs_bitexact(oracle, N, nranks, degree):
-    """M^-1 r on row-block slabs: the temporal-blocked Chebyshev passes take
-    a deep halo (L lines of every pass input from each neighbour) and give the
-    single-grid result bit for bit; slabs thinner than 4 lines (16 / 5) take
-    the per-sweep kernels, also bit-exact."""
+    """M^-1 r on row-block slabs: the temporal-blocked Chebyshev pass (one pass
+    of L = k <= 8 levels) takes a deep halo (L lines of its input from each
+    neighbour) and gives the single-grid result bit for bit; when any slab is
+    thinner than L lines (16 / 5 at degree >= 4, 20 / 4 at degree 6 and 8) every
+    rank takes the per-sweep kernels with one-line halos, also bit-exact."""
     import gmres_amd as ga
 
     r = np.random.default_rng(N + degree).standard_normal(N * N)
@@ -203,6 +204,53 @@ def test_comm_latency_local_group_and_single():
         for t in th:
             t.join(timeout=120)
         assert all(o is not None and o["allreduce_us"] > 0 and o["halo_us"] > 0 for o in out), out
+    finally:
+        for c in ctxs:
+            c.close()
+        g.close()
+
+
+@pytest.mark.parametrize("transport", ["local", "xchg"])
+@pytest.mark.parametrize("degree", [2, 8])
+def test_chebyshev_uneven_slabs_bitexact(oracle, transport, degree):
+    """Any consecutive slabs, not only slab_partition's: a 2-line slab between
+    wide ones.  The temporal-blocked pass needs L lines of every neighbour, so
+    the smallest slab of ANY rank (gathered once over the communicator) decides
+    for all ranks together: degree 2 keeps the fused pass (2 >= L = 2), degree 8
+    drops every rank to the per-sweep kernels.  Bit-exact against the oracle
+    either way, through the in-process group and the device exchange."""
+    import gmres_amd as ga
+
+    N = 40
+    parts = [(0, 19), (19, 2), (21, 19)]
+    r = np.random.default_rng(degree).standard_normal(N * N)
+    ref = oracle.precond(oracle.PREC_CHEB, r, N, params=(8.2, 0.2), degree=degree)
+    g = ga.LocalGroup(3)
+    ctxs = [ga.Context(N, 8, line0=l0, nlines=nl) for l0, nl in parts]
+    out, err = [None] * 3, []
+    try:
+        for q, c in enumerate(ctxs):
+            c.comm_init_local(g, q, 19)
+        if transport == "xchg":
+            for c in ctxs:
+                c.xchg_local()
+        for c in ctxs:
+            c.set_precond("cheb", (8.2, 0.2), degree)
+
+        def work(q):
+            try:
+                l0, nl = parts[q]
+                out[q] = ctxs[q].apply(r[l0 * N:(l0 + nl) * N], 1)
+            except Exception as e:  # pragma: no cover - reported below
+                err.append(e)
+
+        th = [threading.Thread(target=work, args=(q,)) for q in range(3)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=60)
+        assert not err, err
+        assert np.array_equal(np.concatenate(out), ref)
     finally:
         for c in ctxs:
             c.close()

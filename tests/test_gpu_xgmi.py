@@ -278,3 +278,80 @@ def test_comm_latency_diagnostic(nranks):
         assert all(np.array_equal(res[0].hist_res, r.hist_res) for r in res)
     finally:
         _close(g, ctxs)
+
+
+# ------------------------------------------------ a straggling process ------
+
+def _straggler_worker(rank, delay_s, timeout_ms, hq, hin, outq, done):
+    import time
+
+    try:
+        import gmres_amd as ga
+        from gmres_amd import _native as nat
+
+        N, m = 64, 16
+        l0, nl = ga.slab_partition(N, 2)[rank]
+        c = ga.Context(N, m, device=0, line0=l0, nlines=nl)
+        c.comm_init_xgmi(2, rank, N // 2)
+        hq.put((rank, c.xchg_handle()))
+        c.xchg_open(hin.get(timeout=100))
+        c.tune(nat.GK_TUNE_RES_SHARE, 2)
+        c.tune(nat.GK_TUNE_RES, 1)  # the step is one resident launch with in-launch rank totals
+        c.tune(nat.GK_TUNE_XCHG_TIMEOUT_MS, timeout_ms)
+        c.tune(nat.GK_TUNE_RES_TIMEOUT_MS, timeout_ms)
+        ok = c.xchg_selftest(10000)
+        c.set_rhs_ones()
+        c.mgs_cycle_start()  # collective: both ranks in step here
+        time.sleep(delay_s)
+        t0 = time.perf_counter()
+        try:
+            c.mgs_step(1)
+            res = ("no error", time.perf_counter() - t0)
+        except nat.GkError as e:
+            res = (str(e), time.perf_counter() - t0)
+        outq.put((rank, "ok", (ok, res)))
+        done.wait(120)  # keep the exchange region mapped until the peer is done with it
+        c.close()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        outq.put((rank, "error", repr(e)))
+
+
+def test_straggling_process_is_named_within_the_deadline():
+    """Two IPC-connected processes (the multi-GPU transport); rank 1 starts its
+    first Arnoldi step 2 s after the 1.5 s deadline of every exchange wait.
+    Rank 0 must fail that step with GK_ERR_COMM naming rank 1 within the
+    deadline (no GPU hang); rank 1, arriving late, finds rank 0 gone inside the
+    resident launch and fails naming rank 0; both processes exit cleanly and
+    the GPU still solves afterwards."""
+    timeout_ms, delay = 1500, 3.5
+    ctx = mp.get_context("spawn")
+    hq, outq, done = ctx.Queue(), ctx.Queue(), ctx.Event()
+    hins = [ctx.Queue() for _ in range(2)]
+    ps = [ctx.Process(target=_straggler_worker, args=(r, [0.0, delay][r], timeout_ms, hq, hins[r], outq, done))
+          for r in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        hs = dict(hq.get(timeout=100) for _ in range(2))
+        for q in hins:
+            q.put([hs[0], hs[1]])
+        got = dict((r, (kind, val)) for r, kind, val in (outq.get(timeout=100) for _ in range(2)))
+    finally:
+        done.set()
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert [p.exitcode for p in ps] == [0, 0]
+    for r in range(2):
+        assert got[r][0] == "ok", got[r]
+        assert got[r][1][0], "the exchange self-test passed before the straggling"
+    msg0, t0 = got[0][1][1]
+    msg1, t1 = got[1][1][1]
+    assert "status -6" in msg0 and "rank 1" in msg0, msg0
+    assert timeout_ms / 1e3 * 0.9 < t0 < timeout_ms / 1e3 + 1.5, (t0, msg0)  # one deadline, not one per wait
+    assert "status -6" in msg1 and "rank 0" in msg1, msg1
+    assert t1 < timeout_ms / 1e3 + 1.5, (t1, msg1)
+    # the device is healthy: a fresh solve converges as before
+    r = _single(32, 10, "mgsr", "identity", 1, 100)
+    assert r.hist_res[-1] < 1e-12

@@ -1,0 +1,59 @@
+"""Which resident kernel every production split selects (gk_res_plan_query,
+host-only: no GPU touched).
+
+The single-GPU bench runs the w-only kernel (k_mgs_wres); the row-block splits
+of the north-star grid over 2 / 4 / 8 GPUs, and config 4 (8192^2 over 8), give
+each GPU a smaller slab and select the two-array kernels (k_mgs_res<12, L2>).
+The -m gpu tests in tests/test_gpu_splits.py run exactly these variants with
+two ranks on ONE GPU, each rank holding 128 workgroups (GK_TUNE_RES_SHARE 2)
+and a slab chosen so that every workgroup carries the production split's
+chunk load; this table pins that correspondence.
+"""
+import pytest
+
+import gmres_amd as ga
+from gmres_amd import _native
+
+
+def _plan(N, R, share=1, hh=False, nt=-1):
+    nl = max(n for _, n in ga.slab_partition(N, R))
+    return ga.res_plan_query(N * nl, 256, share, hh, nt)
+
+
+@pytest.mark.parametrize("hh", [False, True])
+@pytest.mark.parametrize("N,R,variant,r2e,l2e,nt", [
+    (4096, 1, "w-only", None, 38, 1),      # the bench line (config 1), config 3 and 5
+    (4096, 2, "pairs+lds", 12, 18, 1),     # 8.4 M unknowns per GPU
+    (4096, 4, "pairs+lds", 12, 4, 0),      # 4.2 M
+    (4096, 8, "pairs", 8, 0, 0),           # 2.1 M
+    (8192, 8, "pairs+lds", 12, 18, 1),     # config 4: 8.4 M per GPU
+    (1024, 1, "prefetch", 5, 0, 0),        # config 2
+])
+def test_production_splits(N, R, variant, r2e, l2e, nt, hh):
+    p = _plan(N, R, hh=hh)
+    assert p["variant"] == variant and p["G"] == 256
+    assert p["l2e"] == l2e and p["nt"] == nt
+    if r2e is not None:
+        assert p["r2e"] == r2e
+    else:  # w-only: 88 (MGS-R) / 90 (reflection chains) register chunks of 256 double2
+        assert p["r2e"] == (90 if hh else 88)
+
+
+@pytest.mark.parametrize("N,prod", [(1448, (4096, 8)), (2048, (4096, 4)), (2896, (4096, 2)), (4096, (4096, 1))])
+def test_two_ranks_on_one_gpu_carry_the_production_load(N, prod):
+    """2 ranks x 128 workgroups on one GPU (the -m gpu split tests): the same
+    variant and the same chunks per workgroup as the production split on 256."""
+    t = _plan(N, 2, share=2)
+    p = _plan(*prod)
+    assert t["G"] == 128 and p["G"] == 256
+    for k in ("variant", "r2e", "l2e"):
+        assert t[k] == p[k], (k, t, p)
+    dt = 256 if p["variant"] == "w-only" else 512
+    # resident double2 per workgroup agree within one chunk (ragged last chunk)
+    assert abs(t["nres2"] / t["G"] - p["nres2"] / p["G"]) <= dt
+
+
+def test_query_rejects_bad_arguments():
+    buf = (_native.c_ll * 12)()
+    assert _native.hip().gk_res_plan_query(1, 256, 1, 0, -1, buf) == -1
+    assert _native.hip().gk_res_plan_query(1 << 20, 0, 1, 0, -1, buf) == -1
