@@ -40,6 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; ~6.3 TB/s achievable)
+FABRIC_REF_GBPS = 8600.0  # Infinity-Cache-resident reads chip-wide (MI355X_MICROARCH.md, indexed-rows table)
 METRIC = "Arnoldi iters/sec + HBM GB/s, 4096² Poisson-2D fp64, GMRES(m=95)"
 
 
@@ -350,6 +351,26 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int) -> dict
             "alg_as_written_bytes_per_launch": round(written / launches),
             "alg_as_written_frac": round(written / secs / 1e9 / HBM_PEAK_GBPS, 4),
             "timing": timing, "per_kernel_ms_sampled": {k: round(v[0], 3) for k, v in prof.items()}}
+    if prof.get("res", (0.0, 0))[1] > 0 and args.method == "mgsr":
+        # Which ceiling binds: the fused bytes cross the L2 <-> Infinity Fabric
+        # boundary, but V_i (the AXPY column) is the previous pass's dot column
+        # V_q, read with the default policy so that it is still in the 256 MiB
+        # Infinity Cache: DRAM sees only the dot column of each pass plus w in and
+        # V(:,j+1) out, (16j + 16) n per step launch.  A/B evidence (V_q
+        # non-temporal, so V_i must come from HBM): 41.07 -> 45.06 us per
+        # projection, 5.96 TB/s of HBM traffic = the achievable HBM rate
+        # (profiles/r03/ab_qnt_r03d.jsonl, MI355X_MICROARCH.md 6.0-6.3 TB/s).
+        dram = sum((16.0 * j + 16.0) * nloc for j in steps_js)
+        roof["ceiling"] = ("fabric: L2 <-> Infinity Fabric read rate (Infinity-Cache hits included); the DRAM "
+                           "side carries about half of the fused bytes")
+        roof["fabric"] = {"achieved": roof["achieved"], "peak_ref": FABRIC_REF_GBPS,
+                          "frac": round(roof["achieved"] / FABRIC_REF_GBPS, 4),
+                          "peak_source": "MI355X_MICROARCH.md: Infinity-Cache-resident reads 8.6 TB/s chip-wide"}
+        roof["dram"] = {"bytes_per_launch_est": round(dram / launches), "achieved": round(dram / secs / 1e9, 1),
+                        "frac": round(dram / secs / 1e9 / HBM_PEAK_GBPS, 4),
+                        "model": "(16 j + 16) n per step: each pass's dot column from HBM, its AXPY column from the "
+                                 "Infinity Cache; w in, V(:,j+1) out",
+                        "evidence": "profiles/r03/ab_qnt_r03d.jsonl (V_q non-temporal: +9.7 % per projection)"}
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     key = f"{args.grid}_{m}_{args.prec}_{args.method}_{world}_res"
     if os.path.exists(tf) and prof.get("res", (0, 0))[1] > 0 and args.method == "mgsr":

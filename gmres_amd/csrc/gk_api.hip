@@ -912,100 +912,30 @@ int op_precond(gk_ctx *c, const double *v, double *out, bool resid, int acc, con
     return precond_sweeps(c, out, acc, vdot, part);
 }
 
-#ifndef GK_CF_JT
-#define GK_CF_JT 64  // 64: JT chosen per pass (cf_grid); any other value: that JT (A/B builds)
-#endif
-
-// Grid of a Chebyshev pass: windows of CF_PTS - 2H points across, JT grid
-// lines per workgroup.  A workgroup marches JT + 2L + 1 lines (the recompute
-// cone), so JT is chosen to minimise  rounds x (JT + 2L + 1)  where a round is
-// one wave of resident workgroups (the kernel's occupancy x CUs): at 4096^2,
-// L = 8 (252 VGPRs, 2 waves per SIMD) JT = 80 gives 1924 workgroups in ONE
-// round where 64 would need two.
-template <typename K>
-dim3 cf_grid(gk_ctx *c, K kern, int L, int &JT) {
-    const int H = L + (L & 1);
-    const int gx = (c->N + (gk::CF_PTS - 2 * H) - 1) / (gk::CF_PTS - 2 * H);
-    // the occupancy query once per (kernel, device): every Arnoldi step launches a pass
-    static std::mutex mu;
-    static std::vector<std::pair<std::pair<const void *, int>, int>> seen;
-    int occ = 0;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        const auto key = std::make_pair(reinterpret_cast<const void *>(kern), c->dev);
-        for (const auto &e : seen)
-            if (e.first == key) occ = e.second;
-        if (occ == 0) {
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, gk::CF_W, 0) != hipSuccess || occ <= 0)
-                occ = 8;
-            seen.emplace_back(key, occ);
-        }
-    }
-    const i64 cap = (i64)occ * std::max(1, c->res_cus > 0 ? c->res_cus : 256);
-    static const int jts[] = {16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 256, 384, 512, 1024, 2048, 4096, 8192};
-    // sized by the largest slab, so every rank writes the same number of
-    // partials (the all-reduced slab has one length on all ranks)
-    const int lines = (c->nranks > 1 && c->max_lines > c->nlines) ? c->max_lines : c->nlines;
-    i64 best = -1;
-    JT = GK_CF_JT;
-    for (int jt : jts) {
-        if (GK_CF_JT != 64 && jt != GK_CF_JT) continue;  // a fixed JT (A/B builds)
-        const i64 gy = (lines + jt - 1) / jt, nb = (i64)gx * gy;
-        if (nb > gk::NPMAX) continue;
-        const i64 cost = ((nb + cap - 1) / cap) * (jt + 2 * L + 1);
-        if (best < 0 || cost < best) {
-            best = cost;
-            JT = jt;
-        }
-        if (jt >= lines) break;
-    }
-    // No candidate kept the partial count within a reduction slot (a fixed-JT A/B
-    // build, or gx > NPMAX): grow JT until it does -- a larger grid would write
-    // past its slot into the next one.
-    while (best < 0 && (i64)gx * ((lines + JT - 1) / JT) > gk::NPMAX && JT < lines) JT *= 2;
-    return dim3(gx, (lines + JT - 1) / JT, 1);
-}
-
-template <int L, bool FIRST, bool LAST>
-int launch_cf_acc(gk_ctx *c, int acc, gk::CFArgs &a, i64 *np) {
-    int JT;
-    dim3 g;
-    if (acc == gk::ACC_DOT) {
-        g = cf_grid(c, gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_DOT>, L, JT);
-        if ((i64)g.x * g.y > gk::NPMAX) return set_err(GK_ERR_ARG, "Chebyshev pass grid exceeds a reduction slot");
-        a.JT = JT;
-        gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_DOT><<<g, gk::CF_W, 0, c->st>>>(a);
-    } else if (acc == gk::ACC_NORM) {
-        g = cf_grid(c, gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NORM>, L, JT);
-        if ((i64)g.x * g.y > gk::NPMAX) return set_err(GK_ERR_ARG, "Chebyshev pass grid exceeds a reduction slot");
-        a.JT = JT;
-        gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NORM><<<g, gk::CF_W, 0, c->st>>>(a);
-    } else {
-        g = cf_grid(c, gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NONE>, L, JT);
-        a.JT = JT;
-        gk::k_cheb_fused<L, FIRST, LAST, gk::ACC_NONE><<<g, gk::CF_W, 0, c->st>>>(a);
-    }
-    LAUNCHCHK();
-    if (np != nullptr) *np = (i64)g.x * g.y;
+// One temporal-blocked pass (gk_cheb.hip), tiles sized by the largest slab so
+// every rank writes the same number of partials (the all-reduced slab has one
+// length on all ranks).
+template <bool FIRST, bool LAST>
+int launch_cf(gk_ctx *c, int L, int acc, gk::CFArgs &a, i64 *np) {
+    gk::CFLaunch q{};
+    q.L = L;
+    q.first = FIRST;
+    q.last = LAST;
+    q.acc = acc;
+    q.lines = (c->nranks > 1 && c->max_lines > c->nlines) ? c->max_lines : c->nlines;
+    q.cus = c->res_cus > 0 ? c->res_cus : 256;
+    q.dev = c->dev;
+    q.st = c->st;
+    const int e = gk::cheb_launch(q, a, np);
+    if (e == gk::GK_CF_ESLOT) return set_err(GK_ERR_ARG, "Chebyshev pass grid exceeds a reduction slot");
+    if (e == gk::GK_CF_ESPILL)
+        return set_err(GK_ERR_HIP, "Chebyshev pass (L = %d) was built with a register spill to scratch; refused", L);
+    if (e != 0) return set_err(GK_ERR_HIP, "Chebyshev pass launch: %s", hipGetErrorString((hipError_t)e));
     return GK_OK;
 }
 
-template <bool FIRST, bool LAST>
-int launch_cf(gk_ctx *c, int L, int acc, gk::CFArgs &a, i64 *np) {
-    switch (L) {
-        case 1: return launch_cf_acc<1, FIRST, LAST>(c, acc, a, np);
-        case 2: return launch_cf_acc<2, FIRST, LAST>(c, acc, a, np);
-        case 3: return launch_cf_acc<3, FIRST, LAST>(c, acc, a, np);
-        case 4: return launch_cf_acc<4, FIRST, LAST>(c, acc, a, np);
-        case 5: return launch_cf_acc<5, FIRST, LAST>(c, acc, a, np);
-        case 6: return launch_cf_acc<6, FIRST, LAST>(c, acc, a, np);
-        case 7: return launch_cf_acc<7, FIRST, LAST>(c, acc, a, np);
-        default: return launch_cf_acc<8, FIRST, LAST>(c, acc, a, np);
-    }
-}
-
-// Chebyshev(k <= 8) as one or two temporal-blocked passes (k_cheb_fused):
-// sweeps 1..min(k,4) in the first, the rest in the second.
+// Chebyshev(k <= 16) as one or two temporal-blocked passes (gk_cheb.hip):
+// sweeps 1..min(k, 8) in the first, the rest in the second.
 int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part, const double *c1,
                const double *c2, double theta) {
     ProfScope ps(c, GK_KID_PREC);
@@ -1091,12 +1021,15 @@ int ensure_min_lines(gk_ctx *c) {
     return GK_OK;
 }
 
-// Temporal-blocked Chebyshev passes: even N (two points per lane), k <= 8,
-// and on slabs every rank holding at least the pass's L lines (the deep halo
-// comes from the immediate neighbour only).  The same answer on every rank.
+// Temporal-blocked Chebyshev passes: even N (two points per lane), k <= 16,
+// slabs below 2 GiB per vector, and on slabs every rank holding at least the
+// pass's L lines (the deep halo comes from the immediate neighbour only).  The
+// same answer on every rank.
 int cheb_fused_ok(gk_ctx *c, bool *ok) {
     *ok = false;
     if (!c->tune_cheb_fused || c->N % 2 != 0 || c->pdeg > 2 * gk::CF_LMAX) return GK_OK;
+    // the pass addresses slab vectors through 32-bit buffer offsets
+    if ((i64)c->N * std::max(c->nlines, c->max_lines) * 8 >= (1LL << 31)) return GK_OK;
     if (!collective(c) || c->nranks == 1) {
         *ok = true;
         return GK_OK;

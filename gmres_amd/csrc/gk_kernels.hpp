@@ -17,43 +17,10 @@
 // the CPU oracle (same association order as the Fortran reference); only the
 // dot-product summation order differs.
 #pragma once
-#include <hip/hip_runtime.h>
-#include <type_traits>
+#include "gk_common.hpp"
+#include "gk_cheb.hpp"
 
 namespace gk {
-
-constexpr int TPB = 256;          // threads per workgroup (4 wave64)
-constexpr int WAVES = TPB / 64;
-constexpr int UNR = 4;            // double2 per thread per trip in the streaming kernels
-constexpr int NPMAX = 4096;       // max partials in a slab
-
-typedef long long i64;
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-// Deterministic block sum; result returned to every thread.
-__device__ __forceinline__ double block_sum(double v, double *sm) {
-    v = wave_sum(v);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    __syncthreads();
-    if (lane == 0) sm[wid] = v;
-    __syncthreads();
-    double r = sm[0];
-#pragma unroll
-    for (int k = 1; k < WAVES; ++k) r += sm[k];
-    return r;
-}
-
-// Fixed-order reduction of a partial slab (length np <= NPMAX).
-__device__ __forceinline__ double reduce_slab(const double *__restrict__ p, int np, double *sm) {
-    double s = 0.0;
-    for (int k = threadIdx.x; k < np; k += TPB) s += p[k];
-    return block_sum(s, sm);
-}
 
 // --------------------------------------------------------------------------
 // Projection kernel: the MGS-R / Householder inner cascade
@@ -399,7 +366,6 @@ enum {
     OP_CHEB_FIRST = 3, // x = r: d0 = r/theta; first Chebyshev iteration
     OP_CHEB_ITER = 4,  // x = d: next Chebyshev iteration
 };
-enum { ACC_NONE = 0, ACC_DOT = 1, ACC_NORM = 2 };
 
 struct StArgs {
     const double *x;    // operand, nlines*N
@@ -677,273 +643,6 @@ __global__ __launch_bounds__(TPB) void k_hh_rebuild_upd(double *__restrict__ Vb,
 }  // namespace gk
 
 namespace gk {
-
-// --------------------------------------------------------------------------
-// Temporal blocking of the Chebyshev(k) sweeps (single slab): L sweeps of
-//   res' = res - A d ;  d' = c1 d + c2 res' ;  z' = z + d'
-// in ONE pass.  A workgroup is one wave owning a 128-point window of the fast
-// index i (an L-point halo each side is recomputed, 128 - 2L points are kept)
-// and marching down grid lines with an L-level register pipeline: each time
-// step one input line enters; level l consumes the line level l-1 emitted in
-// the same step, keeps a 3-line window of d plus the (res, z) of its middle
-// line, and emits its middle line.  Per point the arithmetic is exactly the
-// per-sweep kernel's (bit-identical), only the schedule differs: the group
-// moves ~3 vectors in and 3 out instead of 6 per sweep.
-// --------------------------------------------------------------------------
-constexpr int CF_W = 64;           // lanes per window (one wave)
-constexpr int CF_PTS = CF_W * 2;   // points per window (2 per lane)
-constexpr int CF_LMAX = 8;   // Chebyshev(8) = ONE pass
-
-struct CFArgs {
-    const double *din;   // FIRST: z (the residual r); else d entering the group
-    const double *rin;   // !FIRST: residual entering the group
-    const double *zin;   // !FIRST: running sum entering the group
-    double *dout, *rout, *zout;  // !LAST outputs
-    double *out;         // LAST output (the preconditioned vector)
-    const double *vdot;  // ACC_DOT partner
-    double *part;
-    double theta;        // FIRST: d0 = r / theta
-    double c1[CF_LMAX], c2[CF_LMAX];
-    int N, nlines, JT;
-    // Row-block slabs (deep halo): L grid lines of each input from the slab
-    // neighbours -- lo[*] = rows -L..-1, hi[*] = rows nlines..nlines+L-1 --
-    // or nullptr at the physical boundary.  Index 0: din, 1: rin, 2: zin.
-    const double *lo[3], *hi[3];
-};
-
-// Input prefetch depth: lines t+1 .. t+D are in flight while line t runs
-// through the levels (a D-slot ring).  The time loop is unrolled by CF_U = 6
-// steps, the least common multiple of the 3-line window of d, the 2-line
-// (res, z) pair and the ring, so that every rotation of the per-level state is
-// a renaming of registers instead of v_mov copies (with a 4-step unroll the
-// rotations cost ~60 64-bit moves per step).  The dot partner of the emitted
-// line rides in the same ring, so no load issued in the current step is waited
-// on before the step ends.
-#ifndef GK_CF_DEPTH
-#define GK_CF_DEPTH 3
-#endif
-constexpr int CF_U = 6;
-constexpr int CF_D = GK_CF_DEPTH;
-static_assert(CF_U % CF_D == 0, "the ring must rotate a whole number of times per unrolled trip");
-
-// One time step of the level pipeline.  MASK = false: every point of the window
-// and every row any level computes lies inside the grid (or a neighbour's deep
-// halo) -- no per-point selects.  MASK = true (edge windows, the first / last
-// steps of the bottom / top workgroups): rows and points outside the grid are
-// forced to zero at every level, as the per-sweep kernel's boundary does.
-// Both compute every point with the same instructions, so results are
-// identical whichever body a step runs in.
-template <int L, bool FIRST, bool LAST, int ACC>
-__global__ __launch_bounds__(CF_W, 2) void k_cheb_fused(CFArgs a) {
-    constexpr int H = L + (L & 1);                  // halo, even so a lane's 2 points are kept together
-    constexpr int D = CF_D;
-    const int N = a.N;
-    const int lane = threadIdx.x;
-    const int keep = CF_PTS - 2 * H;
-    const i64 ob = (i64)blockIdx.x * keep;          // first kept point
-    const i64 i0 = ob - H + 2 * lane;               // this lane's points i0, i0+1 (i0 even, N even)
-    const bool in0 = i0 >= 0 && i0 < N, in1 = i0 + 1 >= 0 && i0 + 1 < N;
-    const bool kept = (2 * lane >= H) && (2 * lane < CF_PTS - H) && i0 < N;
-    const bool interior = ob - H >= 0 && ob - H + CF_PTS <= N;  // uniform: no lane outside the grid
-    const int j0 = blockIdx.y * a.JT;
-    const int j1 = min(j0 + a.JT, a.nlines);
-    double acc = 0.0;
-    // per-level state: 3-line window of d, (res, z) of the middle and newest lines
-    double dw[L][3][2], rm[L][2], zm[L][2], rn[L][2], zn[L][2];
-#pragma unroll
-    for (int l = 0; l < L; ++l)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            dw[l][0][k] = dw[l][1][k] = dw[l][2][k] = 0.0;
-            rm[l][k] = zm[l][k] = rn[l][k] = zn[l][k] = 0.0;
-        }
-    // rows of the slab, or of a neighbour's deep halo (rows -L.. / nlines..)
-    const bool has_lo = a.lo[0] != nullptr, has_hi = a.hi[0] != nullptr;
-    auto ld2 = [&](int which, const double *base, int row, double (&v)[2]) {
-        v[0] = v[1] = 0.0;
-        const double *p;
-        if (row < 0) {
-            if (!has_lo || row < -L) return;
-            p = a.lo[which] + (i64)(row + L) * N + i0;
-        } else if (row >= a.nlines) {
-            if (!has_hi || row >= a.nlines + L) return;
-            p = a.hi[which] + (i64)(row - a.nlines) * N + i0;
-        } else {
-            p = base + (i64)row * N + i0;
-        }
-        if (in0 && in1) {
-            const double2 t = *reinterpret_cast<const double2 *>(p);
-            v[0] = t.x;
-            v[1] = t.y;
-        }
-    };
-    // the ring: input line `row` and the dot partner of the line the last
-    // level emits when that input enters (row - L)
-    double pd[D][2], pr[D][2], pz[D][2];
-    double2 pv[D];
-    auto issue = [&](int row, int s) {
-        ld2(0, a.din, row, pd[s]);
-        if (!FIRST) {
-            ld2(1, a.rin, row, pr[s]);
-            ld2(2, a.zin, row, pz[s]);
-        }
-        if (LAST && ACC == ACC_DOT) {
-            pv[s] = double2{0.0, 0.0};
-            if (row - L >= j0 && row - L < j1 && kept)
-                pv[s] = *reinterpret_cast<const double2 *>(a.vdot + (i64)(row - L) * N + i0);
-        }
-    };
-    // FAST steps: the ring refills from rows inside the slab, so no row / halo /
-    // lane tests; the dot partner row (t + D - L) lies in the grid then too and
-    // is loaded for every lane (only kept rows of [j0, j1) use it).
-    auto issue_fast = [&](int row, int s) {
-        const double2 t = *reinterpret_cast<const double2 *>(a.din + (i64)row * N + i0);
-        pd[s][0] = t.x;
-        pd[s][1] = t.y;
-        if (LAST && ACC == ACC_DOT) pv[s] = *reinterpret_cast<const double2 *>(a.vdot + (i64)(row - L) * N + i0);
-    };
-    const int tb0 = j0 - L - 1, tend = j1 + L;
-    auto step = [&](auto maskc, int t, int s) {
-        constexpr bool MASK = decltype(maskc)::value;
-        // emission of "level -1": the input line t (slot s), then slot s
-        // refills with line t + D
-        double ed[2], er[2], ez[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            ed[k] = pd[s][k];
-            er[k] = FIRST ? 0.0 : pr[s][k];
-            ez[k] = FIRST ? 0.0 : pz[s][k];
-        }
-        double2 vd = double2{0.0, 0.0};
-        if (LAST && ACC == ACC_DOT) vd = pv[s];
-        if (MASK || !FIRST) {
-            if (t + D < tend) issue(t + D, s);
-        } else {
-            issue_fast(t + D, s);
-        }
-        if (FIRST) {
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const double raw = ed[k];
-                ed[k] = raw / a.theta;
-                er[k] = raw;
-                ez[k] = ed[k];
-            }
-        }
-        int row = t;  // row of the current emission
-#pragma unroll
-        for (int l = 0; l < L; ++l) {
-            // push the emission into level l
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                dw[l][0][k] = dw[l][1][k];
-                dw[l][1][k] = dw[l][2][k];
-                dw[l][2][k] = ed[k];
-                rm[l][k] = rn[l][k];
-                zm[l][k] = zn[l][k];
-                rn[l][k] = er[k];
-                zn[l][k] = ez[k];
-            }
-            // compute the middle line row-1
-            const int mrow = row - 1;
-            const double left = __shfl_up(dw[l][1][1], 1, 64);
-            const double right = __shfl_down(dw[l][1][0], 1, 64);
-            // (MASK) a row outside the GRID is zero at every level (rows in a
-            // neighbour's halo are real; the deepest ones are wrong but never
-            // reach the kept rows -- the usual L-row recompute cone)
-            const bool rowok = !MASK || ((has_lo || mrow >= 0) && (has_hi || mrow < a.nlines));
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const double W = (k == 0) ? left : dw[l][1][0];
-                const double E = (k == 1) ? right : dw[l][1][1];
-                const double s2 = ((W + E) + dw[l][2][k]) + dw[l][0][k];
-                const double ad = 4.0 * dw[l][1][k] - 1.0 * s2;
-                const double res = rm[l][k] - ad;
-                const double dn = a.c1[l] * dw[l][1][k] + a.c2[l] * res;
-                const double z = zm[l][k] + dn;
-                if constexpr (MASK) {
-                    const bool ok = rowok && (k == 0 ? in0 : in1);
-                    ed[k] = ok ? dn : 0.0;
-                    er[k] = ok ? res : 0.0;
-                    ez[k] = ok ? z : 0.0;
-                } else {
-                    ed[k] = dn;
-                    er[k] = res;
-                    ez[k] = z;
-                }
-            }
-            row = mrow;
-        }
-        // the last level emitted line `row`
-        if (row >= j0 && row < j1 && kept) {
-            const i64 idx = (i64)row * N + i0;
-            if (LAST) {
-                *reinterpret_cast<double2 *>(a.out + idx) = double2{ez[0], ez[1]};
-                if (ACC == ACC_DOT) {
-                    acc = acc + ez[0] * vd.x;
-                    acc = acc + ez[1] * vd.y;
-                } else if (ACC == ACC_NORM) {
-                    acc = acc + ez[0] * ez[0];
-                    acc = acc + ez[1] * ez[1];
-                }
-            } else {
-                *reinterpret_cast<double2 *>(a.dout + idx) = double2{ed[0], ed[1]};
-                *reinterpret_cast<double2 *>(a.rout + idx) = double2{er[0], er[1]};
-                *reinterpret_cast<double2 *>(a.zout + idx) = double2{ez[0], ez[1]};
-            }
-        }
-        // Keep the scheduler from interleaving consecutive steps: across a step
-        // boundary only 4 doubles per point and level are live (d of the two
-        // newest lines, res and z of the newest), and hoisting the next step's
-        // work over the boundary pushes the wave past 256 registers (spills)
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    if (j0 < a.nlines) {
-#pragma unroll
-        for (int s = 0; s < D; ++s)
-            if (tb0 + s < tend) issue(tb0 + s, s);
-        // Steps [ts0, ts1) compute no row outside the grid at any level: level l
-        // computes row t - l - 1, so rows >= 0 need t >= L and rows < nlines
-        // need t <= nlines (without the neighbour's halo on that side).  A FAST
-        // trip also refills the ring from slab rows only: t + D in [0, nlines).
-        // The trips run as three loops -- masked prologue [tb0, tf0), FAST
-        // [tf0, tf1), masked epilogue [tf1, tend) -- with every boundary a whole
-        // number of CF_U-step trips from tb0 (the ring slots stay compile-time).
-        // Separate loops, not a branch per trip: with both bodies behind one
-        // branch the compiler hoists their common arithmetic above it and spills.
-        const int ts0 = max(has_lo ? tb0 : L, -D), ts1 = min(has_hi ? tend : a.nlines + 1, a.nlines - D);
-        int tf0 = tend, tf1 = tend;
-        if (interior) {
-            const int lo = max(ts0, tb0), hi = min(ts1, tend);
-            const int f0 = tb0 + (lo - tb0 + CF_U - 1) / CF_U * CF_U;
-            const int nf = hi > f0 ? (hi - f0) / CF_U : 0;
-            if (nf > 0) {
-                tf0 = f0;
-                tf1 = f0 + nf * CF_U;
-            }
-        }
-#pragma nounroll
-        for (int seg = 0; seg < 3; ++seg) {
-            if (seg == 1) {
-                for (int tb = tf0; tb < tf1; tb += CF_U) {
-#pragma unroll
-                    for (int u = 0; u < CF_U; ++u) step(std::false_type{}, tb + u, u % D);
-                }
-            } else {
-                const int ta = seg == 0 ? tb0 : tf1, tz = seg == 0 ? tf0 : tend;
-                for (int tb = ta; tb < tz; tb += CF_U) {
-#pragma unroll
-                    for (int u = 0; u < CF_U; ++u)
-                        if (tb + u < tz) step(std::true_type{}, tb + u, u % D);
-                }
-            }
-        }
-    }
-    if (ACC != ACC_NONE) {
-        const double s = wave_sum(acc);
-        if (lane == 0) a.part[(i64)blockIdx.y * gridDim.x + blockIdx.x] = s;
-    }
-}
 
 // --------------------------------------------------------------------------
 // Device-initiated exchange between ranks (the "xgmi" collective back-end).
@@ -1863,6 +1562,13 @@ constexpr int TOUCH_MGS = GK_RES_TOUCH_MGS;
 #define GK_RES_ROT 0
 #endif
 constexpr int RES_ROT = GK_RES_ROT;
+// Load policy of the dot column V_q of a pass (A/B knob): 0 = default, so the
+// column is still in the Infinity Cache when the next pass reads it as its
+// AXPY column V_i; 1 = non-temporal like V_i (every column comes from HBM).
+#ifndef GK_RES_QNT
+#define GK_RES_QNT 0
+#endif
+constexpr bool RES_QNT = GK_RES_QNT != 0;
 #ifndef GK_RES_TOUCH_PACE
 #define GK_RES_TOUCH_PACE 24
 #endif
@@ -1953,7 +1659,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             const i64 c = c0 + u;
             if (u < RW && c < cend) {
                 pa[u] = ldv<true>(A2 + c * WT + t);
-                if (dot) pb[u] = B2[c * WT + t];
+                if (dot) pb[u] = ldv<RES_QNT>(B2 + c * WT + t);
             }
         }
     };
@@ -1976,7 +1682,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                     bv[u] = pb[u];
                 } else if (k0 + u < RW && c < cend) {
                     av[u] = ldv<true>(A2 + c * WT + t);
-                    if (dot) bv[u] = B2[c * WT + t];
+                    if (dot) bv[u] = ldv<RES_QNT>(B2 + c * WT + t);
                 }
             }
 #pragma unroll
@@ -1997,7 +1703,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 const i64 c = l0 + k0 + u;
                 if (k0 + u < LW && c < lend) {
                     av[u] = ldv<true>(A2 + c * WT + t);
-                    if (dot) bv[u] = B2[c * WT + t];
+                    if (dot) bv[u] = ldv<RES_QNT>(B2 + c * WT + t);
                 }
             }
 #pragma unroll
@@ -2020,7 +1726,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 if (e < n2) {
                     wv[u] = W2[e];
                     av[u] = ldv<true>(A2 + e);
-                    if (dot) bv[u] = B2[e];
+                    if (dot) bv[u] = ldv<RES_QNT>(B2 + e);
                 }
             }
 #pragma unroll

@@ -51,15 +51,19 @@ def test_poisson5_slabs_with_halos(oracle, N, nranks):
         assert np.array_equal(ys.cpu().numpy(), ref[line0 * N:(line0 + nl) * N])
 
 
-PREC_CASES = [("cbpr2", 1), ("identity", 1)] + [("cheb", k) for k in range(1, 9)]
+PREC_CASES = [("cbpr2", 1), ("identity", 1)] + [("cheb", k) for k in range(1, 9)] + [("cheb", 11), ("cheb", 16)]
 
 
-@pytest.mark.parametrize("N", [16, 64, 129, 130, 256])
+@pytest.mark.parametrize("N", [16, 64, 126, 128, 129, 130, 256, 372])
 @pytest.mark.parametrize("kind,degree", PREC_CASES)
 def test_precond_bitexact(oracle, N, kind, degree):
     """Every Chebyshev degree 1..8: ONE temporal-blocked pass of L = k levels
-    (k <= CF_LMAX = 8) when N is even; 130 and 256 have more than one line tile
-    (ragged last tile at 130); odd N takes the per-sweep kernels."""
+    (k <= CF_LMAX = 8) when N is even; degrees 11 and 16 run two passes (8 + 3,
+    8 + 8: the (d, res, z) hand-over).  N < 128 is the one-window SMALL variant
+    (lanes beyond N held at zero), 128 one window whose both edges are the
+    grid's, 130 / 256 / 372 two to four windows (the last one aligned to the
+    grid's E edge, overlapping its neighbour's halo) and more than one line
+    tile; odd N takes the per-sweep kernels."""
     import gmres_amd.solver as S
 
     rng = np.random.default_rng(N + degree)
@@ -114,7 +118,7 @@ def _ctx_col(c, k):
     return c.get_x()
 
 
-@pytest.mark.parametrize("N,degree", [(130, 3), (256, 6), (256, 8)])
+@pytest.mark.parametrize("N,degree", [(130, 3), (256, 6), (256, 8), (1024, 8), (4096, 8)])
 def test_fused_chebyshev_norm_epilogue(oracle, N, degree):
     """The ACC_NORM last pass (cycle start: w = M^-1 b, beta = ||w||, V(:,1) = w/beta):
     w is bit-exact, so V(:,1) equals oracle_w / beta_gpu bit for bit, and beta is
@@ -136,7 +140,7 @@ def test_fused_chebyshev_norm_epilogue(oracle, N, degree):
         assert np.array_equal(v1, w / beta)
 
 
-@pytest.mark.parametrize("N,degree", [(130, 5), (256, 8)])
+@pytest.mark.parametrize("N,degree", [(130, 5), (256, 8), (1024, 8), (2048, 8), (4096, 8)])
 def test_fused_chebyshev_dot_epilogue_step(N, degree):
     """The ACC_DOT last pass inside an Arnoldi step (w = M^-1 A V(:,j) fused with
     <w, V(:,1)>): fused passes vs per-sweep kernels give the same Hessenberg

@@ -96,3 +96,20 @@ def test_product_does_not_import_oracle():
                 txt = open(os.path.join(dirpath, f)).read()
                 for bad in ("import oracle", "from oracle", "liboracle", "gmres_oracle", "or_gmres", "or_stvec"):
                     assert bad not in txt, (f, bad)
+
+
+def test_build_refuses_chebyshev_scratch_spills():
+    """gmres_amd/build.py parses the resource-usage remarks of the Chebyshev
+    translation units and fails the build when any k_cheb_fused instantiation
+    spills registers to scratch (gk_cheb.hip refuses such kernels at run time
+    too: a spilled build gave wrong results past two unrolled trips)."""
+    from gmres_amd import build as b
+
+    remarks = ("gk_cheb.hip:46:1: remark: Function Name: _ZN2gk12k_cheb_fusedILi8ELb1ELb1ELi1ELb0EEEvNS_6CFArgsE\n"
+               "gk_cheb.hip:46:1: remark:     ScratchSize [bytes/lane]: 16 [-Rpass-analysis=kernel-resource-usage]\n"
+               "gk_cheb.hip:46:1: remark: Function Name: _ZN2gk12k_cheb_fusedILi4ELb1ELb1ELi1ELb0EEEvNS_6CFArgsE\n"
+               "gk_cheb.hip:46:1: remark:     ScratchSize [bytes/lane]: 0 [-Rpass-analysis=kernel-resource-usage]\n"
+               "gk_api.hip:9:1: remark: Function Name: _ZN2gk6k_projILi0ELb1ELi2EEEvPdPKdS3_\n"
+               "gk_api.hip:9:1: remark:     ScratchSize [bytes/lane]: 32 [-Rpass-analysis=kernel-resource-usage]\n")
+    assert b._scratch_kernels(remarks, "k_cheb_fused") == ["_ZN2gk12k_cheb_fusedILi8ELb1ELb1ELi1ELb0EEEvNS_6CFArgsE"]
+    assert [u[2] for u in b.HIP_UNITS] == ["gk_api.o"] + [f"gk_cheb{p}.o" for p in range(b.GK_CF_PARTS)]

@@ -41,7 +41,8 @@ def main() -> None:
             roof = d.get("roofline") or {}
             row = {"variant": v, "round": r, "value": d["value"], "ms_per_step": d["ms_per_step"],
                    "per_projection_us": roof.get("per_projection_us"), "frac": roof.get("frac"),
-                   "resid": d["check"]["true_rel_residual_after_timed_cycles"], "fallback": d.get("fallback")}
+                   "resid": d["check"]["true_rel_residual_after_timed_cycles"], "fallback": d.get("fallback"),
+                   "split": ((d.get("diagnostics") or {}).get("resident_split_per_unit_us"))}
             res[v].append(row)
             print(json.dumps(row), flush=True)
     summ = {v: {"median_it_s": statistics.median([x["value"] for x in rows]),

@@ -4,7 +4,9 @@
 // per workgroup.  Pattern "mgs": a(p) = p, b(p) = p+1 -- B of pass p is A of
 // pass p+1 (the resident step's V_q -> V_i reuse).  Pattern "fresh": b(p) =
 // p+48 -- no column is read twice within 48 passes.  Policies: A non-temporal
-// or default; B default.  Pattern "one": only A (single-stream bandwidth).
+// or default; B default or non-temporal (does a non-temporal load still leave
+// the line in the Infinity Cache for the next pass?).  Pattern "one": only A
+// (single-stream bandwidth).
 // Prints microseconds per pass (median of the timed passes) and GB/s.
 //   hipcc --offload-arch=gfx950 -O3 tools/mall_probe.hip -o tools/mall_probe
 #include <hip/hip_runtime.h>
@@ -29,7 +31,7 @@ __device__ __forceinline__ double2 ld_nt(const double2 *p) {
     return double2{t.x, t.y};
 }
 
-template <bool NT_A, bool TWO>
+template <bool NT_A, bool NT_B, bool TWO>
 __global__ __launch_bounds__(256) void k_pass(const double2 *__restrict__ A, const double2 *__restrict__ B,
                                               long long n2, double *__restrict__ out) {
     double acc = 0.0;
@@ -41,7 +43,7 @@ __global__ __launch_bounds__(256) void k_pass(const double2 *__restrict__ A, con
             const long long e = e0 + u * stride;
             if (e < n2) {
                 a[u] = NT_A ? ld_nt(A + e) : A[e];
-                b[u] = TWO ? B[e] : double2{1.0, 1.0};
+                b[u] = TWO ? (NT_B ? ld_nt(B + e) : B[e]) : double2{1.0, 1.0};
             } else {
                 a[u] = b[u] = double2{0.0, 0.0};
             }
@@ -68,9 +70,11 @@ int main(int argc, char **argv) {
     struct Case {
         const char *name;
         int reuse;  // b = a + reuse
-        bool nt, two;
-    } cases[] = {{"mgs_ntA", 1, true, true},  {"mgs_defA", 1, false, true}, {"fresh_ntA", 48, true, true},
-                 {"fresh_defA", 48, false, true}, {"one_nt", 0, true, false}, {"one_def", 0, false, false}};
+        bool nt, ntb, two;
+    } cases[] = {{"mgs_ntA", 1, true, false, true},     {"mgs_ntAB", 1, true, true, true},
+                 {"mgs_defA", 1, false, false, true},   {"fresh_ntA", 48, true, false, true},
+                 {"fresh_ntAB", 48, true, true, true},  {"fresh_defA", 48, false, false, true},
+                 {"one_nt", 0, true, false, false},     {"one_def", 0, false, false, false}};
     for (const Case &c : cases) {
         std::vector<float> t;
         for (int p = 0; p < passes; ++p) {
@@ -78,11 +82,12 @@ int main(int argc, char **argv) {
             const double2 *B = V + (long long)((p + c.reuse) % ncol) * n2;
             CK(hipEventRecord(e0, 0));
             if (c.two) {
-                if (c.nt) k_pass<true, true><<<blocks, 256>>>(A, B, n2, out);
-                else k_pass<false, true><<<blocks, 256>>>(A, B, n2, out);
+                if (c.nt && c.ntb) k_pass<true, true, true><<<blocks, 256>>>(A, B, n2, out);
+                else if (c.nt) k_pass<true, false, true><<<blocks, 256>>>(A, B, n2, out);
+                else k_pass<false, false, true><<<blocks, 256>>>(A, B, n2, out);
             } else {
-                if (c.nt) k_pass<true, false><<<blocks, 256>>>(A, B, n2, out);
-                else k_pass<false, false><<<blocks, 256>>>(A, B, n2, out);
+                if (c.nt) k_pass<true, false, false><<<blocks, 256>>>(A, B, n2, out);
+                else k_pass<false, false, false><<<blocks, 256>>>(A, B, n2, out);
             }
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
