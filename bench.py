@@ -73,10 +73,12 @@ def prec_bytes(n: int, prec: str, degree: int, model: str) -> float:
     if prec == "cbpr2":
         return float(64 * n if model == "as_written" else 16 * n)
     # Chebyshev(k): 48n per sweep as written; fused, k <= 8 sweeps are ONE
-    # temporal-blocked pass (read z, write the result: 16n; its dot partner is
-    # the stencil launch's); each further pass of up to 8 hands over (d, r, z): +48n
+    # temporal-blocked pass whose stage 0 is the stencil itself (reads v, writes
+    # the result, reads the dot partner: the 24n the stencil term already
+    # counts, so +0); each further pass of up to 8 hands over (d, r, z): +48n
+    # (and the first pass then runs after a stencil launch: +16n)
     passes = (degree + 7) // 8
-    return float(48 * degree * n if model == "as_written" else (16 + 48 * (passes - 1)) * n)
+    return float(48 * degree * n if model == "as_written" else (0 if passes == 1 else 16 + 48 * (passes - 1)) * n)
 
 
 def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str) -> float:

@@ -91,7 +91,7 @@ struct gk_ctx {
     double *V = nullptr;  // (m+1) columns, stride ld
     double *w = nullptr, *z = nullptr, *aux = nullptr, *dA = nullptr, *dB = nullptr;
     double *x = nullptr, *b = nullptr, *vj = nullptr, *hlo = nullptr, *hhi = nullptr;
-    double *dh = nullptr;  // deep halos of the Chebyshev pass inputs: [3 vectors][lo, hi][CF_LMAX lines][N]
+    double *dh = nullptr;  // deep halos of the Chebyshev pass inputs: [3 vectors][lo, hi][CF_HMAX lines][N]
     double *red = nullptr;   // NSLOT * NPMAX partial slabs
     double *hcol = nullptr;  // m+2 Hessenberg column / scalars
     double *ydev = nullptr;  // m+1
@@ -153,6 +153,7 @@ struct gk_ctx {
     int np_st = 0, np_pj = 0, nblk_stream = 0;
     int last_np = 0;          // partial count written by the last ACC-carrying sweep
     int tune_cheb_fused = 1;  // temporal-blocked Chebyshev sweeps (single slab)
+    int tune_cheb_sten = 1;   // the Arnoldi step's pass forms z = A v itself (stage 0)
     // tuning knobs (gk_set_tuning)
     int tune_nt = -1, tune_pj_blocks = 0, tune_st_blocks = 0;  // tune_nt: -1 auto
     bool nt_auto = false;
@@ -892,8 +893,15 @@ int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *
 // out = M^-1 (A v)  or  out = M^-1 (b - A v) (resid); the LAST sweep carries
 // the fused reduction `acc` (dot with vdot, or norm) into slab `part`.
 // Reference: gmres_mgsr.f90:336-337 (step), :314-320 (cycle start).
+int op_precond_sten(gk_ctx *c, const double *v, double *out, int acc, const double *vdot, double *part,
+                    bool *done);
 int op_precond(gk_ctx *c, const double *v, double *out, bool resid, int acc, const double *vdot,
                double *part) {
+    if (!resid) {
+        bool done = false;
+        CHK(op_precond_sten(c, v, out, acc, vdot, part, &done));
+        if (done) return GK_OK;
+    }
     CHK(halo(c, v));
     gk::StArgs a{};
     if (c->pkind == GK_PREC_IDENTITY) {
@@ -912,13 +920,38 @@ int op_precond(gk_ctx *c, const double *v, double *out, bool resid, int acc, con
     return precond_sweeps(c, out, acc, vdot, part);
 }
 
+// The Arnoldi step's out = M^-1 (A v) with Chebyshev(k <= 8) as ONE pass whose
+// stage 0 forms z = A v itself: no stencil launch, no z vector (the pass reads
+// v; on slabs v brings k + 1 deep-halo lines).  *done = false: not applicable
+// (the caller takes the stencil + pass route).
+int cheb_fused_ok(gk_ctx *c, bool *ok);
+int cheb_coefs(gk_ctx *c, double *c1, double *c2, double *theta);
+int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part, const double *c1,
+               const double *c2, double theta, const double *sten_v);
+int op_precond_sten(gk_ctx *c, const double *v, double *out, int acc, const double *vdot, double *part,
+                    bool *done) {
+    *done = false;
+    if (c->pkind != GK_PREC_CHEB || acc != gk::ACC_DOT || !c->tune_cheb_sten || c->pdeg > gk::CF_LMAX ||
+        c->N < gk::CF_PTS)
+        return GK_OK;
+    bool fused = false;
+    CHK(cheb_fused_ok(c, &fused));
+    if (!fused || (collective(c) && c->nranks > 1 && c->min_lines < c->pdeg + 1)) return GK_OK;
+    double c1[2 * gk::CF_LMAX], c2[2 * gk::CF_LMAX], theta;
+    CHK(cheb_coefs(c, c1, c2, &theta));
+    CHK(cheb_fused(c, out, acc, vdot, part, c1, c2, theta, v));
+    *done = true;
+    return GK_OK;
+}
+
 // One temporal-blocked pass (gk_cheb.hip), tiles sized by the largest slab so
 // every rank writes the same number of partials (the all-reduced slab has one
 // length on all ranks).
 template <bool FIRST, bool LAST>
-int launch_cf(gk_ctx *c, int L, int acc, gk::CFArgs &a, i64 *np) {
+int launch_cf(gk_ctx *c, int L, int acc, gk::CFArgs &a, i64 *np, bool sten = false) {
     gk::CFLaunch q{};
     q.L = L;
+    q.sten = sten;
     q.first = FIRST;
     q.last = LAST;
     q.acc = acc;
@@ -928,6 +961,7 @@ int launch_cf(gk_ctx *c, int L, int acc, gk::CFArgs &a, i64 *np) {
     q.st = c->st;
     const int e = gk::cheb_launch(q, a, np);
     if (e == gk::GK_CF_ESLOT) return set_err(GK_ERR_ARG, "Chebyshev pass grid exceeds a reduction slot");
+    if (e == gk::GK_CF_ESTEN) return set_err(GK_ERR_ARG, "fused-stencil Chebyshev pass outside its variants");
     if (e == gk::GK_CF_ESPILL)
         return set_err(GK_ERR_HIP, "Chebyshev pass (L = %d) was built with a register spill to scratch; refused", L);
     if (e != 0) return set_err(GK_ERR_HIP, "Chebyshev pass launch: %s", hipGetErrorString((hipError_t)e));
@@ -937,15 +971,16 @@ int launch_cf(gk_ctx *c, int L, int acc, gk::CFArgs &a, i64 *np) {
 // Chebyshev(k <= 16) as one or two temporal-blocked passes (gk_cheb.hip):
 // sweeps 1..min(k, 8) in the first, the rest in the second.
 int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part, const double *c1,
-               const double *c2, double theta) {
+               const double *c2, double theta, const double *sten_v) {
     ProfScope ps(c, GK_KID_PREC);
     const int k = c->pdeg;
     const int g1 = std::min(k, gk::CF_LMAX), g2 = k - g1;
+    const bool sten = sten_v != nullptr;  // one pass (k <= 8) taking v, stage 0 = the stencil
     // On slabs every input of a pass brings L lines of each neighbour (deep halo).
     const bool slabs = collective(c) && c->nranks > 1;
     const bool has_lo = slabs && c->rank > 0, has_hi = slabs && c->rank < c->nranks - 1;
-    auto dlo = [&](int v) { return c->dh + (i64)(2 * v) * gk::CF_LMAX * c->N; };
-    auto dhi = [&](int v) { return c->dh + (i64)(2 * v + 1) * gk::CF_LMAX * c->N; };
+    auto dlo = [&](int v) { return c->dh + (i64)(2 * v) * gk::CF_HMAX * c->N; };
+    auto dhi = [&](int v) { return c->dh + (i64)(2 * v + 1) * gk::CF_HMAX * c->N; };
     auto deep = [&](gk::CFArgs &x, int v, const double *vec, int L) -> int {
         if (slabs) CHK(halo_lines(c, vec, L, dlo(v), dhi(v)));
         x.lo[v] = has_lo ? dlo(v) : nullptr;
@@ -956,10 +991,10 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
     a.N = c->N;
     a.nlines = c->nlines;
     a.theta = theta;
-    a.din = c->z;
+    a.din = sten ? sten_v : c->z;
     a.vdot = vdot;
     a.part = part;
-    CHK(deep(a, 0, c->z, g1));
+    CHK(deep(a, 0, a.din, g1 + (sten ? 1 : 0)));
     for (int l = 0; l < g1; ++l) {
         a.c1[l] = c1[l];
         a.c2[l] = c2[l];
@@ -967,7 +1002,7 @@ int cheb_fused(gk_ctx *c, double *out, int acc, const double *vdot, double *part
     i64 np = 0;
     if (g2 == 0) {
         a.out = out;
-        CHK((launch_cf<true, true>(c, g1, acc, a, &np)));
+        CHK((launch_cf<true, true>(c, g1, acc, a, &np, sten)));
         if (acc != gk::ACC_NONE) c->last_np = (int)np;
         return GK_OK;
     }
@@ -1039,6 +1074,21 @@ int cheb_fused_ok(gk_ctx *c, bool *ok) {
     return GK_OK;
 }
 
+// Chebyshev(k) coefficients of the sweeps (the per-sweep kernels' recurrence).
+int cheb_coefs(gk_ctx *c, double *c1, double *c2, double *theta) {
+    *theta = (c->p0 + c->p1) / 2.0;
+    const double delta = std::fabs(c->p1 - c->p0) / 2.0;
+    const double sigma = *theta / delta;
+    double rho0 = delta / *theta;
+    for (int it = 0; it < c->pdeg; ++it) {
+        const double rho1 = 1.0 / (2.0 * sigma - rho0);
+        c1[it] = rho1 * rho0;
+        c2[it] = 2.0 * rho1 / delta;
+        rho0 = rho1;
+    }
+    return GK_OK;
+}
+
 // out = M^-1 z for z already in c->z (cbpr2 or Chebyshev sweeps).
 int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *part) {
     bool fused = false;
@@ -1069,14 +1119,9 @@ int precond_sweeps(gk_ctx *c, double *out, int acc, const double *vdot, double *
     const double sigma = theta / delta;
     double rho0 = delta / theta;
     if (fused) {
-        double c1[2 * gk::CF_LMAX], c2[2 * gk::CF_LMAX];
-        for (int it = 0; it < c->pdeg; ++it) {
-            const double rho1 = 1.0 / (2.0 * sigma - rho0);
-            c1[it] = rho1 * rho0;
-            c2[it] = 2.0 * rho1 / delta;
-            rho0 = rho1;
-        }
-        return cheb_fused(c, out, acc, vdot, part, c1, c2, theta);
+        double c1[2 * gk::CF_LMAX], c2[2 * gk::CF_LMAX], th;
+        CHK(cheb_coefs(c, c1, c2, &th));
+        return cheb_fused(c, out, acc, vdot, part, c1, c2, th, nullptr);
     }
     double *dcur = c->dA, *dnext = c->dB;
     for (int it = 0; it < c->pdeg; ++it) {
@@ -1244,7 +1289,7 @@ int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out)
         if (hipMalloc(p, vb) != hipSuccess) return fail(set_err(GK_ERR_NOMEM, "cannot allocate work vectors"));
     if (hipMalloc(&c->hlo, sizeof(double) * nside) != hipSuccess ||
         hipMalloc(&c->hhi, sizeof(double) * nside) != hipSuccess ||
-        hipMalloc(&c->dh, sizeof(double) * 6 * gk::CF_LMAX * (size_t)nside) != hipSuccess ||
+        hipMalloc(&c->dh, sizeof(double) * 6 * gk::CF_HMAX * (size_t)nside) != hipSuccess ||
         hipMalloc(&c->red, sizeof(double) * NSLOT * gk::NPMAX) != hipSuccess ||
         hipMalloc(&c->hcol, sizeof(double) * (m + 2)) != hipSuccess ||
         hipMalloc(&c->ydev, sizeof(double) * (m + 1)) != hipSuccess ||
@@ -2084,6 +2129,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_RES_LDS: c->tune_res_lds = value != 0; break;
         case GK_TUNE_RES_WONLY: c->tune_res_wonly = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_HH_FUSE: c->tune_hh_fuse = value != 0; break;
+        case GK_TUNE_CHEB_STEN: c->tune_cheb_sten = value != 0; break;
         case GK_TUNE_VERR_ORDER: c->tune_verr_order = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");

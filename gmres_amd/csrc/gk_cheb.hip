@@ -42,9 +42,15 @@ constexpr int CF_D = GK_CF_DEPTH;  // input lines in flight
 constexpr int CF_OCC = GK_CF_OCC;  // waves per SIMD the register budget is cut for
 static_assert(CF_U % CF_D == 0, "the ring must rotate a whole number of times per unrolled trip");
 
-template <int L, bool FIRST, bool LAST, int ACC, bool SMALL>
+template <int L, bool FIRST, bool LAST, int ACC, bool SMALL, bool STEN>
 __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF_OCC))) void k_cheb_fused(CFArgs a) {
-    constexpr int H = cf_halo(L);
+    // STEN (first pass only): the input is the Krylov column v and a stage 0
+    // ahead of the levels forms the pass's z = A v row by row (the stencil
+    // launch's arithmetic), so the step needs no stencil launch and no z vector
+    static_assert(!STEN || (FIRST && !SMALL), "the fused stencil stage is a first-pass, full-window variant");
+    constexpr int S0 = STEN ? 1 : 0;
+    constexpr int LL = L + S0;                      // pipeline stages: the recompute cone and halo
+    constexpr int H = cf_halo(LL);
     constexpr int D = CF_D;
     const int N = a.N;
     const int lane = threadIdx.x;
@@ -93,7 +99,10 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
     // a level reads its z before the level above overwrites it with the new
     // line's (a wave's LDS operations complete in order).
     double d[L][3][2], r[L][2][2];
+    double vw[3][2];  // STEN: three lines of v
     __shared__ double2 zs[L][CF_W];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) vw[q][0] = vw[q][1] = 0.0;
 #pragma unroll
     for (int l = 0; l < L; ++l) {
 #pragma unroll
@@ -114,10 +123,10 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
         v[0] = v[1] = 0.0;
         const double *p;
         if (row < 0) {
-            if (!has_lo || row < -L) return;
-            p = a.lo[which] + (i64)(row + L) * N + i0;
+            if (!has_lo || row < -LL) return;
+            p = a.lo[which] + (i64)(row + LL) * N + i0;
         } else if (row >= a.nlines) {
-            if (!has_hi || row >= a.nlines + L) return;
+            if (!has_hi || row >= a.nlines + LL) return;
             p = a.hi[which] + (i64)(row - a.nlines) * N + i0;
         } else {
             p = base + (i64)row * N + i0;
@@ -154,7 +163,7 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
             pv[s] = *reinterpret_cast<const double2 *>(a.vdot + (i64)row * N + i0);
         }
     };
-    const int tb0 = j0 - L, tend = j1 + L;
+    const int tb0 = j0 - LL, tend = j1 + LL;
 
     // One time step t (phase U of the unrolled trip).  FAST: every level
     // computes a row inside the grid (or a neighbour's halo) that reaches the
@@ -165,15 +174,45 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
         constexpr int SS = U % 3, SC = (U + 1) % 3, SN = (U + 2) % 3;  // d slots: rows R-2, R-1, R
         constexpr int QC = (U + 1) % 2, QN = U % 2;                     // (res, z) slots: R-1, R
         constexpr int RS = U % D;                                       // ring slot of line t
-        // level -1 emits the input line t into level 0's incoming slots
+        // level -1 emits the input line t into level 0's incoming slots (STEN:
+        // stage 0 takes line t of v and emits z = A v of line t - 1)
+        if (STEN) {
+            vw[SN][0] = pd[RS][0];
+            vw[SN][1] = pd[RS][1];
+            const int srow = t - 1;
+            bool zero = false, run = true;
+            if (!FAST) {
+                zero = (!has_lo && srow < 0) || (!has_hi && srow >= a.nlines);
+                run = !zero && srow >= j0 - L && srow < j1 + L;
+            }
+            // values first, then unconditional stores into the state (stores in
+            // the branches get merged through a pointer phi, which keeps the
+            // state arrays out of registers)
+            double nd0 = d[0][SN][0], nd1 = d[0][SN][1], nr0 = r[0][QN][0], nr1 = r[0][QN][1];
+            if (zero) {
+                nd0 = nd1 = 0.0;
+            } else if (run) {
+                const double C0 = vw[SC][0], C1 = vw[SC][1];
+                const double W0 = cf_from_left(C1), E1 = cf_from_right(C0);
+                const double s0 = ((W0 + C1) + vw[SN][0]) + vw[SS][0];
+                const double s1 = ((C0 + E1) + vw[SN][1]) + vw[SS][1];
+                const double ax0 = 4.0 * C0 - 1.0 * s0, ax1 = 4.0 * C1 - 1.0 * s1;
+                nd0 = ax0 / a.theta;
+                nd1 = ax1 / a.theta;
+                nr0 = ax0;
+                nr1 = ax1;
+            }
+            d[0][SN][0] = nd0, d[0][SN][1] = nd1, r[0][QN][0] = nr0, r[0][QN][1] = nr1;
+        } else {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (FIRST) {
-                d[0][SN][k] = pd[RS][k] / a.theta;
-                r[0][QN][k] = pd[RS][k];
-            } else {
-                d[0][SN][k] = pd[RS][k];
-                r[0][QN][k] = pr[RS][k];
+            for (int k = 0; k < 2; ++k) {
+                if (FIRST) {
+                    d[0][SN][k] = pd[RS][k] / a.theta;
+                    r[0][QN][k] = pd[RS][k];
+                } else {
+                    d[0][SN][k] = pd[RS][k];
+                    r[0][QN][k] = pr[RS][k];
+                }
             }
         }
         // z of the line level 0 computes now; then the input line's z takes its place
@@ -186,7 +225,7 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
         double od[2] = {0.0, 0.0}, orr[2] = {0.0, 0.0}, oz[2] = {0.0, 0.0};  // the last level's emission
 #pragma unroll
         for (int l = 0; l < L; ++l) {
-            const int row = t - l - 1;  // the row level l computes
+            const int row = t - l - 1 - S0;  // the row level l computes
             // read ahead the z level l+1 consumes in this step, before this level
             // writes the z of its new line in its place
             const double2 znext = (l + 1 < L) ? zs[l + 1][lane] : double2{0.0, 0.0};
@@ -226,8 +265,8 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
             zcur = znext;
             if (CF_LVBAR) __builtin_amdgcn_sched_barrier(0);
         }
-        // the last level emitted row t - L
-        const int orow = t - L;
+        // the last level emitted row t - LL
+        const int orow = t - LL;
         if ((FAST || (orow >= j0 && orow < j1)) && kept) {
             const i64 idx = (i64)orow * N + i0;
             if (LAST) {
@@ -246,7 +285,7 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
             }
         }
         // the partner of the row emitted D steps from now
-        if (FAST || t + D < tend) issue_dot(FAST, t + D - L, RS);
+        if (FAST || t + D < tend) issue_dot(FAST, t + D - LL, RS);
         // keep the scheduler from hoisting the next step's work over this one
         // (only the 4 doubles per point and level above are live across it)
         __builtin_amdgcn_sched_barrier(0);
@@ -265,13 +304,13 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
 #pragma unroll
         for (int s = 0; s < D; ++s) {
             issue_in(false, tb0 + s, s);
-            issue_dot(false, tb0 + s - L, s);
+            issue_dot(false, tb0 + s - LL, s);
         }
-        // FAST steps: t >= j0 + L (every level's row reaches the kept rows),
-        // rows t-L..t-1 inside the grid unless a neighbour's halo covers them,
+        // FAST steps: t >= j0 + LL (every stage's row reaches the kept rows),
+        // rows t-LL..t-1 inside the grid unless a neighbour's halo covers them,
         // ring refills t + D inside the slab.  Segment boundaries are whole
         // trips from tb0, so every ring / state slot stays compile-time.
-        const int lo = j0 + L;
+        const int lo = j0 + LL;
         const int hi = min(min(tend, a.nlines - D), has_hi ? tend : a.nlines + 1);
         int tf0 = tend, tf1 = tend;
         const int f0 = tb0 + (max(lo, tb0) - tb0 + CF_U - 1) / CF_U * CF_U;
@@ -347,14 +386,14 @@ int pick_jt(int gx, int lines, int L, i64 cap) {
     return JT;
 }
 
-template <int L, bool FIRST, bool LAST, int ACC, bool SMALL>
+template <int L, bool FIRST, bool LAST, int ACC, bool SMALL, bool STEN = false>
 int launch(const CFLaunch &q, CFArgs &a, i64 *np) {
-    auto kern = k_cheb_fused<L, FIRST, LAST, ACC, SMALL>;
-    const int gx = cf_windows(a.N, L);
+    auto kern = k_cheb_fused<L, FIRST, LAST, ACC, SMALL, STEN>;
+    const int gx = cf_windows(a.N, L + (STEN ? 1 : 0));
     const int occ = occupancy(kern, q.dev);
     if (occ == 0) return GK_CF_ESPILL;
     const i64 cap = (i64)occ * (q.cus > 0 ? q.cus : 256);
-    const int JT = pick_jt(gx, q.lines, L, cap);
+    const int JT = pick_jt(gx, q.lines, L + (STEN ? 1 : 0), cap);
     const dim3 g(gx, (q.lines + JT - 1) / JT, 1);
     if (ACC != ACC_NONE && (i64)g.x * g.y > NPMAX) return GK_CF_ESLOT;
     a.JT = JT;
@@ -372,6 +411,12 @@ int launch(const CFLaunch &q, CFArgs &a, i64 *np) {
 // translation units (the unrolled kernels dominate the build time).
 template <int L, bool FIRST, bool LAST>
 int cf_launch_acc(const CFLaunch &q, CFArgs &a, i64 *np) {
+    if constexpr (FIRST && LAST) {
+        if (q.sten) {  // the Arnoldi step's pass with its stencil: ACC_DOT, full windows only
+            if (q.acc != ACC_DOT || a.N < CF_PTS) return GK_CF_ESTEN;
+            return launch<L, true, true, ACC_DOT, false, true>(q, a, np);
+        }
+    }
     const bool small = a.N < CF_PTS;
     if (q.acc == ACC_DOT)
         return small ? launch<L, FIRST, LAST, ACC_DOT, true>(q, a, np) : launch<L, FIRST, LAST, ACC_DOT, false>(q, a, np);

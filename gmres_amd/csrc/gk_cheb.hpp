@@ -38,6 +38,7 @@ namespace gk {
 constexpr int CF_W = 64;           // lanes per window (one wave)
 constexpr int CF_PTS = CF_W * 2;   // points per window (2 per lane)
 constexpr int CF_LMAX = 8;         // Chebyshev(8) = ONE pass
+constexpr int CF_HMAX = CF_LMAX + 1;  // deepest halo: a pass with the fused stencil stage
 
 struct CFArgs {
     const double *din;   // FIRST: z (the residual r); else d entering the pass
@@ -76,6 +77,7 @@ struct CFLaunch {
     int L;
     bool first, last;
     int acc;
+    bool sten;  // first pass takes v and forms z = A v itself (ACC_DOT, N >= CF_PTS; deep halo L + 1)
     int lines;  // grid lines the tiles are sized for (the largest slab on N ranks)
     int cus;    // CUs the pass may fill
     int dev;
@@ -83,6 +85,7 @@ struct CFLaunch {
 };
 constexpr int GK_CF_ESLOT = -1;
 constexpr int GK_CF_ESPILL = -2;  // the build spilled the pass's registers to scratch
+constexpr int GK_CF_ESTEN = -3;   // a fused-stencil pass asked for outside its variants
 int cheb_launch(const CFLaunch &q, CFArgs &a, i64 *np);
 
 }  // namespace gk

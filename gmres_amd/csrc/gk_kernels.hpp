@@ -784,7 +784,7 @@ __global__ __launch_bounds__(TPB) void k_xchg(double *__restrict__ buf, int coun
 // Halo lines through the same regions: my first grid line goes to rank-1
 // (its side 1), my last to rank+1 (its side 0); then wait for mine and decode
 // them into hlo / hhi, the buffers the stencil reads.  One thread per point.
-constexpr int XS_HALO_LINES = CF_LMAX;  // deepest halo (the temporal-blocked Chebyshev passes)
+constexpr int XS_HALO_LINES = CF_HMAX;  // deepest halo (the temporal-blocked Chebyshev passes)
 
 __global__ __launch_bounds__(TPB) void k_xhalo(const double *__restrict__ vec, int N, int nlines, int nl,
                                                XsPeers peers, int nranks, int rank, unsigned seq,

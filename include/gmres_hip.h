@@ -320,7 +320,10 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          its small launches into the reflection chains -- the DOWN chain builds
  *                          e_j itself, the UP chain ends with the reflector fix-up and
  *                          P(:,j+1) = w/||w|| (gmres_hh.f90:306-318); 0: separate k_set_unit,
- *                          k_hh_fix and k_scale launches */
+ *                          k_hh_fix and k_scale launches
+ *   GK_TUNE_CHEB_STEN      1 (default): the Arnoldi step's Chebyshev(k <= 8) pass forms z = A v
+ *                          itself in a stage ahead of its levels (no stencil launch, no z vector;
+ *                          N >= 128, slabs of at least k + 1 lines); 0: stencil launch + pass */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
@@ -337,6 +340,7 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_RES_WONLY 13
 #define GK_TUNE_VERR_ORDER 14
 #define GK_TUNE_HH_FUSE 15
+#define GK_TUNE_CHEB_STEN 16
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

@@ -161,3 +161,27 @@ def test_fused_chebyshev_dot_epilogue_step(N, degree):
     for a, b in zip(res[1][0], res[0][0]):
         assert np.allclose(a, b, rtol=1e-12, atol=1e-15)
     assert np.allclose(res[1][1], res[0][1], rtol=1e-10, atol=1e-14)
+
+
+@pytest.mark.parametrize("N,degree", [(130, 5), (1024, 8), (4096, 8)])
+def test_fused_stencil_stage_matches_stencil_launch(N, degree):
+    """GK_TUNE_CHEB_STEN: the Arnoldi step's Chebyshev pass forming z = A v in
+    its stage 0 (no stencil launch) against the stencil launch + pass: the
+    element-wise w is the same arithmetic, so the Hessenberg columns and
+    Krylov vectors of steps 1..4 agree up to the fused dot's summation order
+    (the stage-0 pass has a wider halo, hence another window grid)."""
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+
+    res = {}
+    for sten in (1, 0):
+        with ga.Context(N, 10) as c:
+            c.tune(nat.GK_TUNE_CHEB_STEN, sten)
+            c.set_precond("cheb", (8.2, 0.2), degree)
+            c.set_rhs_ones()
+            c.mgs_cycle_start()
+            cols = [c.mgs_step(j) for j in range(1, 5)]
+            res[sten] = (cols, _ctx_col(c, 4))
+    for a, b in zip(res[1][0], res[0][0]):
+        assert np.allclose(a, b, rtol=1e-12, atol=1e-15)
+    assert np.allclose(res[1][1], res[0][1], rtol=1e-10, atol=1e-14)
