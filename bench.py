@@ -55,10 +55,13 @@ METRIC = "Arnoldi iters/sec + HBM GB/s, 4096² Poisson-2D fp64, GMRES(m=95)"
 #    columns it touches, 16n; per resident step launch (32j + 16) n (2j
 #    projections + reading w once + writing V(:,j+1)).  roofline.frac uses it.
 
-def mgs_step_bytes(n: int, j: int, model: str) -> float:
-    """One resident MGS-R step launch (cascade + norm + scale; the stencil is
-    its own launch)."""
-    return float((80 * j + 24) * n if model == "as_written" else (32 * j + 16) * n)
+def mgs_step_bytes(n: int, j: int, model: str, sten: bool = False) -> float:
+    """One resident MGS-R step launch (cascade + norm + scale).  sten: the launch
+    forms w = A V(:,j) itself and takes the first dot (reads V(:,j) and V(:,1)
+    instead of w: +8n fused); otherwise the stencil is its own launch."""
+    if model == "as_written":
+        return float((80 * j + 24 + (16 if sten else 0)) * n)
+    return float((32 * j + 16 + (8 if sten else 0)) * n)
 
 
 def hh_chain_bytes(n: int, L: int, model: str) -> float:
@@ -81,8 +84,9 @@ def prec_bytes(n: int, prec: str, degree: int, model: str) -> float:
     return float(48 * degree * n if model == "as_written" else (0 if passes == 1 else 16 + 48 * (passes - 1)) * n)
 
 
-def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str) -> float:
-    """One full restart cycle of m Arnoldi steps."""
+def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str, sten: bool = False) -> float:
+    """One full restart cycle of m Arnoldi steps (sten: the step launches form
+    w = A V(:,j) themselves -- the stencil's 24n become the launch's +8n)."""
     if model == "as_written":  # SURVEY 8(d): per step (40 + 80 j) n, cycle start 64n, update 8(m+2)n
         if method == "hh":
             b = sum((64 + 80 * j) * n for j in range(1, m + 1)) + 64 * n + 8 * (m + 2) * n + 40 * m * n
@@ -94,7 +98,7 @@ def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str)
         b = sum(hh_chain_bytes(n, j, model) * 2 + st + 40 * n for j in range(1, m + 1))
         b += hh_chain_bytes(n, m, model) + 24 * n + 40 * n
     else:
-        b = sum(mgs_step_bytes(n, j, model) + st for j in range(1, m + 1))
+        b = sum(mgs_step_bytes(n, j, model, sten) + (0 if sten else st) for j in range(1, m + 1))
         b += 40 * n + 8 * (m + 2) * n  # cycle start (b - A x, norm, V_1) + x update
     return float(b + (m + 1) * prec_bytes(n, prec, degree, model))
 
@@ -307,9 +311,10 @@ def setup_xgmi(ctx, dist, world: int, rank: int, required: bool):
     return None
 
 
-def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int) -> dict | None:
+def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, sten: bool = False) -> dict | None:
     """Dominant kernel: its algorithmic bytes per launch (fused-minimum model)
-    over its average launch time from HIP events on the context stream."""
+    over its average launch time from HIP events on the context stream.  sten:
+    the MGS step launch forms w = A V(:,j) itself (gk_res_info "sten")."""
     m = args.m
     if not prof or prof.get("res", (0.0, 0))[1] == 0:
         if not prof or prof["proj"][1] == 0:
@@ -337,11 +342,12 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int) -> dict
         else:
             S = max(1, args.prof_every)
             steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
-            fused = sum(mgs_step_bytes(nloc, j, "fused") for j in steps_js)
-            written = sum(mgs_step_bytes(nloc, j, "as_written") for j in steps_js)
+            fused = sum(mgs_step_bytes(nloc, j, "fused", sten) for j in steps_js)
+            written = sum(mgs_step_bytes(nloc, j, "as_written", sten) for j in steps_js)
             nproj = sum(2 * j for j in steps_js)
             kname = ("gk::k_mgs_wres / k_mgs_res (resident MGS-R step: 2j fused projections + norm + scale, one "
-                     "persistent launch per Arnoldi step)")
+                     "persistent launch per Arnoldi step" + ("; w = A V(:,j) and the first dot formed in the "
+                                                             "launch's prologue)" if sten else ")"))
             timing = f"HIP events on the context stream around the step launch of steps j % {S} == 0 of the timed cycles"
         per_proj = ms * 1e3 / nproj
     secs = ms / 1e3
@@ -362,7 +368,7 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int) -> dict
         # non-temporal, so V_i must come from HBM): 41.07 -> 45.06 us per
         # projection, 5.96 TB/s of HBM traffic = the achievable HBM rate
         # (profiles/r03/ab_qnt_r03d.jsonl, MI355X_MICROARCH.md 6.0-6.3 TB/s).
-        dram = sum((16.0 * j + 16.0) * nloc for j in steps_js)
+        dram = sum((16.0 * j + 16.0 + (8.0 if sten else 0.0)) * nloc for j in steps_js)
         roof["ceiling"] = ("fabric: L2 <-> Infinity Fabric read rate (Infinity-Cache hits included); the DRAM "
                            "side carries about half of the fused bytes")
         roof["fabric"] = {"achieved": roof["achieved"], "peak_ref": FABRIC_REF_GBPS,
@@ -371,12 +377,14 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int) -> dict
         roof["dram"] = {"bytes_per_launch_est": round(dram / launches), "achieved": round(dram / secs / 1e9, 1),
                         "frac": round(dram / secs / 1e9 / HBM_PEAK_GBPS, 4),
                         "model": "(16 j + 16) n per step: each pass's dot column from HBM, its AXPY column from the "
-                                 "Infinity Cache; w in, V(:,j+1) out",
+                                 "Infinity Cache; w (or, forming w in the launch, V(:,j) and V(:,1)) in, V(:,j+1) out",
                         "evidence": "profiles/r03/ab_qnt_r03d.jsonl (V_q non-temporal: +9.7 % per projection)"}
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     key = f"{args.grid}_{m}_{args.prec}_{args.method}_{world}_res"
     if os.path.exists(tf) and prof.get("res", (0, 0))[1] > 0 and args.method == "mgsr":
         pm = json.load(open(tf)).get(key)
+        if pm and bool(pm.get("sten", False)) != sten:  # measured on the other step flow: not this kernel's bytes
+            pm = None
         if pm and "per_step" in pm:
             per_step = {int(k): v for k, v in pm["per_step"].items()}
             if all(j in per_step for j in set(steps_js)):
@@ -484,7 +492,8 @@ def config_legs(ga, prof_every: int) -> list[dict]:
             c.sync()
             t1 = time.perf_counter()
             prof = c.profile_read()
-            roof = roofline_entry(prof, ns, c.nloc, r.n_cycles, 1) or {}
+            sten = method == "mgsr" and c.res_info().get("sten", 0) == 1
+            roof = roofline_entry(prof, ns, c.nloc, r.n_cycles, 1, sten) or {}
         iters = (r.n_cycles - 1) * m + r.n_out
         pname = {"identity": "no precond", "cbpr2": "cbpr2", "cheb": f"Chebyshev({degree})"}[prec]
         leg = {"baseline_config": idx, "workload": f"{N}x{N} Poisson-2D fp64, GMRES-{method.upper()} m={m}, {pname}",
@@ -528,6 +537,8 @@ def main() -> None:
                     help="HIP events around the launches of every S-th Arnoldi step (1 = all)")
     ap.add_argument("--plan-only", action="store_true", help="print the multi-GPU launch plan and exit")
     ap.add_argument("--no-diag", action="store_true", help="skip the post-timing diagnostic cycle")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="A/B runs: gk_set_tuning(KEY, VALUE) on the bench context (include/gmres_hip.h GK_TUNE_*)")
     args = ap.parse_args()
     maybe_self_launch(args, sys.argv[1:])
 
@@ -570,6 +581,9 @@ def main() -> None:
         collective = "rccl"
     if world > 1 and args.collective in ("auto", "xgmi"):
         collective = setup_xgmi(ctx, dist, world, rank, required=args.collective == "xgmi") or "rccl"
+    for kv in args.tune:
+        k, v = kv.split("=")
+        ctx.tune(int(k), int(v))
     ctx.set_precond(args.prec, (8.2, 0.2), args.degree)
     ctx.set_rhs_ones()
 
@@ -636,7 +650,8 @@ def main() -> None:
     iters = (cycles - 1) * m + res.n_out if cycles > 0 else 0
     diag = None if args.no_diag else diagnostics(ctx, args, run, dist, world)
 
-    roof = roofline_entry(prof, args, ctx.nloc, cycles, world) if rank == 0 else None
+    sten = args.method == "mgsr" and ctx.res_info().get("sten", 0) == 1
+    roof = roofline_entry(prof, args, ctx.nloc, cycles, world, sten) if rank == 0 else None
     ctx.close()
     legs = None
     if rank == 0 and world == 1 and not args.no_configs and (N, m, args.prec, args.method) == (4096, 95, "identity",
@@ -646,8 +661,8 @@ def main() -> None:
         n = N * N
         it_s = iters / elapsed
         full = cycles == args.steps and res.n_out == m
-        b_fused = cycle_bytes(n, m, args.prec, args.degree, args.method, "fused") * cycles
-        b_written = cycle_bytes(n, m, args.prec, args.degree, args.method, "as_written") * cycles
+        b_fused = cycle_bytes(n, m, args.prec, args.degree, args.method, "fused", sten) * cycles
+        b_written = cycle_bytes(n, m, args.prec, args.degree, args.method, "as_written", sten) * cycles
         cpu = None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(N, m, args.prec, args.degree, args.method, args.cpu_cap, args.cpu_cap_leg)

@@ -154,6 +154,7 @@ struct gk_ctx {
     int last_np = 0;          // partial count written by the last ACC-carrying sweep
     int tune_cheb_fused = 1;  // temporal-blocked Chebyshev sweeps (single slab)
     int tune_cheb_sten = 1;   // the Arnoldi step's pass forms z = A v itself (stage 0)
+    int tune_res_sten = 0;    // the w-only MGS step launch forms w = A V(:,j) itself (A/B: slower)
     // tuning knobs (gk_set_tuning)
     int tune_nt = -1, tune_pj_blocks = 0, tune_st_blocks = 0;  // tune_nt: -1 auto
     bool nt_auto = false;
@@ -733,7 +734,7 @@ bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
 }
 
 // gk_res_plan_query / gk_res_info layout
-enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, RPI_R2E, RPI_L2E, RPI_LDS, RPI_NRES2 };
+enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, RPI_R2E, RPI_L2E, RPI_LDS, RPI_NRES2, RPI_STEN };
 void plan_info(const ResPlan &p, bool on, long long *info) {
     for (int k = 0; k < GK_RES_INFO_LEN; ++k) info[k] = 0;
     if (!on) return;
@@ -777,18 +778,18 @@ int launch_res_t(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     }
 }
 
-template <int MODE>
+template <int MODE, bool STEN = false>
 int launch_wres_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     constexpr int RW = MODE == gk::RES_MGS ? RES_RW : RES_RW_HH;
     constexpr int WBT = MODE == gk::RES_MGS ? gk::WB : gk::WB_HH;
     static std::atomic<int> attr[ATTR_DEVS];
     if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
     if (attr[c->dev].load() < p.lds) {
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RW, RES_LW, MODE, WBT>),
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RW, RES_LW, MODE, WBT, STEN>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
         attr[c->dev] = p.lds;
     }
-    gk::k_mgs_wres<RW, RES_LW, MODE, WBT><<<p.G, gk::WT, p.lds, c->st>>>(a);
+    gk::k_mgs_wres<RW, RES_LW, MODE, WBT, STEN><<<p.G, gk::WT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
 }
@@ -797,7 +798,9 @@ int launch_wres(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     switch (a.mode) {
         case gk::RES_HH_UP: return launch_wres_m<gk::RES_HH_UP>(c, p, a);
         case gk::RES_HH_DOWN: return launch_wres_m<gk::RES_HH_DOWN>(c, p, a);
-        default: return launch_wres_m<gk::RES_MGS>(c, p, a);
+        default:
+            return a.sten_v != nullptr ? launch_wres_m<gk::RES_MGS, true>(c, p, a)
+                                       : launch_wres_m<gk::RES_MGS>(c, p, a);
     }
 }
 
@@ -823,13 +826,19 @@ int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 //  flags (w-only variant, p.wo): RESF_CLOSE_HH -- RES_HH_UP also makes P(:,j+1) and
 //    writes w(1:j+1) to c->hb (one more exchange); RESF_UNIT_INIT -- RES_HH_DOWN builds
 //    its unit input e_{unit_g} itself.
+//  sten_v (RES_MGS, w-only variant): the launch forms w = A sten_v itself and the
+//    first dot with it (no pin); the halo lines of sten_v must be in c->hlo / c->hhi.
 enum { RESF_CLOSE_HH = 1, RESF_UNIT_INIT = 2 };
 int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, double *hs, double *hcopy,
-             int mode = gk::RES_MGS, double *w = nullptr, i64 unit_g = -1, int flags = 0) {
+             int mode = gk::RES_MGS, double *w = nullptr, i64 unit_g = -1, int flags = 0,
+             const double *sten_v = nullptr) {
     ProfScope ps(c, GK_KID_RES);
     const bool close = (flags & RESF_CLOSE_HH) && mode == gk::RES_HH_UP;
     if (flags != 0 && !p.wo) return set_err(GK_ERR_STATE, "resident flags %d need the w-only variant", flags);
-    const int np = (mode == gk::RES_MGS ? 2 * j : j) + (close ? 1 : 0);  // exchanges of the launch
+    if (sten_v != nullptr && (!p.wo || mode != gk::RES_MGS || c->N % 2 != 0))
+        return set_err(GK_ERR_STATE, "the stencil prologue needs the w-only MGS step and even N");
+    // exchanges of the launch (the stencil prologue adds the first dot's)
+    const int np = (mode == gk::RES_MGS ? 2 * j : j) + (close ? 1 : 0) + (sten_v != nullptr ? 1 : 0);
     if (c->res_tag > 0xF0000000u) {  // tags must never repeat within the granule region's lifetime
         HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_WORDS, c->st));
         c->res_tag = 1;
@@ -867,6 +876,11 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
         c->res_trace_g = p.G;
         c->res_trace_np = np;
     }
+    a.sten_v = sten_v;
+    a.slo = halo_lo(c);
+    a.shi = halo_hi(c);
+    a.N = c->N;
+    a.nlines = c->nlines;
     a.nranks = 1;
     if (c->xs_on && c->nranks > 1) {
         a.err = c->xs_err_dev;
@@ -878,6 +892,12 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
         c->xs_seq += (unsigned)np;
     }
     return launch_res(c, p, a);
+}
+
+// Does the MGS step's resident launch form w = A V(:,j) itself (GK_TUNE_RES_STEN)?
+// The identity operator with the w-only variant and even N (double2 rows).
+bool res_sten(gk_ctx *c, const ResPlan &p) {
+    return c->tune_res_sten && p.wo && c->pkind == GK_PREC_IDENTITY && c->N % 2 == 0;
 }
 
 int d2h_sync(gk_ctx *c, double *host, const double *dev, int count) {
@@ -1779,11 +1799,20 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
     double *hs = c->hall + (i64)(j - 1) * m2;  // H(1:j+1, j) of this step, on device
     c->prof_on_step = (j % c->prof_every) == 0;
     int s0 = 0, s1 = 1;
+    ResPlan rp;
+    const bool res = res_plan(c, rp);
+    if (res && res_sten(c, rp)) {  // w = A V(:,j), the first dot and the cascade: ONE launch
+        CHK(halo(c, V + (i64)(j - 1) * ld));
+        CHK(res_step(c, j, rp, nullptr, 0, hs, c->hallh_dev + (i64)(j - 1) * m2, gk::RES_MGS, nullptr, -1, 0,
+                     V + (i64)(j - 1) * ld));
+        HIPCHK(hipEventRecord(c->ev_step[j], c->st));
+        c->prof_on_step = true;
+        return GK_OK;
+    }
     // w = M^-1 A V(:,j), fused with the first dot <w, V(:,1)>
     CHK(op_precond(c, V + (i64)(j - 1) * ld, c->w, false, gk::ACC_DOT, V, slot(c, s0)));
     int np = c->last_np;
-    ResPlan rp;
-    if (res_plan(c, rp)) {  // the whole cascade + norm + scale as one resident launch
+    if (res) {  // the whole cascade + norm + scale as one resident launch
         CHK(allreduce(c, slot(c, s0), np));
         CHK(res_step(c, j, rp, slot(c, s0), np, hs, c->hallh_dev + (i64)(j - 1) * m2));
         HIPCHK(hipEventRecord(c->ev_step[j], c->st));
@@ -2130,6 +2159,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_RES_WONLY: c->tune_res_wonly = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_HH_FUSE: c->tune_hh_fuse = value != 0; break;
         case GK_TUNE_CHEB_STEN: c->tune_cheb_sten = value != 0; break;
+        case GK_TUNE_RES_STEN: c->tune_res_sten = value != 0; break;
         case GK_TUNE_VERR_ORDER: c->tune_verr_order = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
@@ -2303,6 +2333,7 @@ int gk_res_info(gk_ctx *c, int hh, long long *info) {
     ResPlan p;
     const bool on = res_plan(c, p, hh != 0);
     plan_info(p, on, info);
+    info[RPI_STEN] = on && hh == 0 && res_sten(c, p) ? 1 : 0;
     return GK_OK;
 }
 

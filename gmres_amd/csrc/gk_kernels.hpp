@@ -893,6 +893,10 @@ struct ResArgs {
     double *hb;           // close_hh: w(1:j+1) before the fix-up, written by the owner rank (pivot input)
     int unit_init;        // RES_HH_DOWN with unit_known: the launch builds e_u itself (w not read)
     u64 *trace;           // gk_profile_res_trace (nullptr = off): [workgroup][RES_TRACE_X][publish, seen] ticks
+    // w-only kernel, RES_MGS with STEN: the launch forms w = A V(:,j) itself
+    const double *sten_v;         // V(:,j)
+    const double *slo, *shi;      // its halo lines -1 / nlines (nullptr: the physical boundary)
+    int N, nlines;                // grid side, slab lines
 };
 constexpr int RES_TRACE_X = 2 * RHMAX + 2;  // exchanges recorded per workgroup (all of one launch)
 
@@ -1590,8 +1594,14 @@ constexpr int TOUCH_PACE = GK_RES_TOUCH_PACE;
 // re-tune (profiles/r02/ab_pace_retune.jsonl): 8 / 24 -> 41.06 / 41.1 vs 40.57 us burst
 constexpr int TOUCH_PACE_HH = GK_RES_TOUCH_PACE_HH;
 
-template <int RW, int LW, int MODE, int WBT = WB>
+// STEN (RES_MGS, identity operator): the launch forms w = A V(:,j) in its
+// prologue -- the stencil launch's arithmetic, ((W+E)+N)+S and 4x - s, element
+// by element from V(:,j) and its halo lines -- and takes the first dot
+// <w, V(:,1)> with it as one more in-launch all-gather, instead of reading w
+// and the partial slab of a separate stencil launch (gmres_mgsr.f90:336,346).
+template <int RW, int LW, int MODE, int WBT = WB, bool STEN = false>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
+    static_assert(!STEN || MODE == RES_MGS, "the stencil prologue is the MGS step's");
     extern __shared__ double2 lw[];  // [LW][WT]
     __shared__ double sm[WT / 64];
     __shared__ double bc[1];
@@ -1630,11 +1640,67 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             if (l0 + k < lend) lw[k * WT + t] = unit2((l0 + k) * WT + t);
         for (i64 e = sbase; e < n2; e += sstride) W2[e] = unit2(e);
         if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.w[a.n - 1] = (a.n - 1 == u) ? 1.0 : 0.0;
-    } else {
+    } else if (!STEN) {
 #pragma unroll
         for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
         for (int k = 0; k < LW; ++k)
             if (l0 + k < lend) lw[k * WT + t] = W2[(l0 + k) * WT + t];
+    }
+    // STEN: w = A V(:,j) at double2 index e2 (local elements 2 e2, 2 e2 + 1; N even)
+    // and the first dot's partial <w, V(:,1)>, batches of SB chunks in flight
+    double sten_acc = 0.0;
+    if constexpr (STEN) {
+        const double *__restrict__ vj = a.sten_v;
+        const double2 *__restrict__ Vj2 = reinterpret_cast<const double2 *>(vj);
+        const double2 *__restrict__ Lo2 = reinterpret_cast<const double2 *>(a.slo);
+        const double2 *__restrict__ Hi2 = reinterpret_cast<const double2 *>(a.shi);
+        const int N = a.N, hN = a.N >> 1, nl = a.nlines;
+        struct Ld {
+            double2 c, up, dn, v1;
+            double l, r;
+        };
+        auto load = [&](i64 e2) {
+            Ld q;
+            const int g = (int)(2 * e2), row = g / N, col = g - row * N;
+            q.c = Vj2[e2];
+            q.l = col > 0 ? vj[g - 1] : 0.0;
+            q.r = col + 2 < N ? vj[g + 2] : 0.0;
+            q.up = row + 1 < nl ? Vj2[e2 + hN] : (Hi2 != nullptr ? Hi2[col >> 1] : double2{0.0, 0.0});
+            q.dn = row > 0 ? Vj2[e2 - hN] : (Lo2 != nullptr ? Lo2[col >> 1] : double2{0.0, 0.0});
+            q.v1 = V2[e2];
+            return q;
+        };
+        auto make = [&](const Ld &q) {
+            const double s0 = ((q.l + q.c.y) + q.up.x) + q.dn.x;
+            const double s1 = ((q.c.x + q.r) + q.up.y) + q.dn.y;
+            const double2 w2 = double2{4.0 * q.c.x - 1.0 * s0, 4.0 * q.c.y - 1.0 * s1};
+            sten_acc = sten_acc + w2.x * q.v1.x;
+            sten_acc = sten_acc + w2.y * q.v1.y;
+            return w2;
+        };
+        constexpr int SB = 4;
+#pragma unroll
+        for (int k0 = 0; k0 < RW; k0 += SB) {
+            Ld q[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u)
+                if (k0 + u < RW && c0 + k0 + u < cend) q[u] = load((c0 + k0 + u) * WT + t);
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int k = k0 + u;
+                if (k < RW) wr[k] = (c0 + k < cend) ? make(q[u]) : double2{0.0, 0.0};
+            }
+        }
+        for (int k0 = 0; k0 < LW; k0 += SB) {
+            Ld q[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u)
+                if (k0 + u < LW && l0 + k0 + u < lend) q[u] = load((l0 + k0 + u) * WT + t);
+#pragma unroll
+            for (int u = 0; u < SB; ++u)
+                if (k0 + u < LW && l0 + k0 + u < lend) lw[(k0 + u) * WT + t] = make(q[u]);
+        }
+        for (i64 e = sbase; e < n2; e += sstride) W2[e] = make(load(e));  // streamed part: to HBM
     }
     // acc += the closing reduction of element pair e2 (local double2 index)
     auto red = [&](double &acc, const double2 &v, const double2 &b, int kind, i64 e2, bool chk) {
@@ -1804,6 +1870,9 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         }
         if (XPF) load_first(q, res_col(mode, j, 1), kind_of(0) == RK_DOT);
         ok = reduce(acc, h, kind_of(0) == RK_DOT ? res_col(mode, j, 1) : -1);
+    } else if constexpr (STEN) {
+        if (XPF) load_first(res_col(mode, j, 0), res_col(mode, j, 1), kind_of(0) == RK_DOT);
+        ok = reduce(sten_acc, h, kind_of(0) == RK_DOT ? res_col(mode, j, 1) : -1);
     } else {
         if (XPF) load_first(res_col(mode, j, 0), res_col(mode, j, 1), kind_of(0) == RK_DOT);
         double s = 0.0;

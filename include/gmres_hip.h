@@ -265,7 +265,8 @@ int gk_sync(gk_ctx *ctx);
  *   GK_RES_WONLY      k_mgs_wres: w only, in registers + LDS (large slabs).
  * info[GK_RES_INFO_LEN]: variant, workgroups G, R2, L2, prefetch, control
  * wave, w-only, non-temporal column loads, register / LDS chunks per
- * workgroup in use, dynamic LDS bytes, resident double2 of the slab.
+ * workgroup in use, dynamic LDS bytes, resident double2 of the slab, and
+ * (gk_res_info only) whether the MGS step launch forms w = A V(:,j) itself.
  * gk_res_plan_query: pure host computation for a slab of nloc unknowns on a
  * device with `cus` compute units shared by `share` contexts; hh != 0 the
  * reflection chains' plan; nt: -1 auto (from nloc), 0 / 1 forced.  No device
@@ -277,7 +278,7 @@ int gk_sync(gk_ctx *ctx);
 #define GK_RES_PAIRS 2
 #define GK_RES_PAIRS_LDS 3
 #define GK_RES_WONLY 4
-#define GK_RES_INFO_LEN 12
+#define GK_RES_INFO_LEN 13
 int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, long long *info);
 int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 
@@ -323,7 +324,12 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          k_hh_fix and k_scale launches
  *   GK_TUNE_CHEB_STEN      1 (default): the Arnoldi step's Chebyshev(k <= 8) pass forms z = A v
  *                          itself in a stage ahead of its levels (no stencil launch, no z vector;
- *                          N >= 128, slabs of at least k + 1 lines); 0: stencil launch + pass */
+ *                          N >= 128, slabs of at least k + 1 lines); 0: stencil launch + pass
+ *   GK_TUNE_RES_STEN       0 (default): stencil launch + resident step; 1: with the identity
+ *                          operator the w-only resident MGS step forms w = A V(:,j) in its prologue
+ *                          and takes the first dot with it (no stencil launch; even N) -- measured
+ *                          4 % slower at 4096^2: the prologue's loads cannot be kept in flight beside
+ *                          the register-resident w */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
@@ -341,6 +347,7 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_VERR_ORDER 14
 #define GK_TUNE_HH_FUSE 15
 #define GK_TUNE_CHEB_STEN 16
+#define GK_TUNE_RES_STEN 17
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

@@ -4,6 +4,7 @@ each variant's bench line is taken in its own process (GK_LIB_DIR selects the
 build), variants interleaved over several rounds so box drift hits all alike.
 
   python tools/ab_lib.py --variants base xpf88 xpf80 --rounds 2 -- --steps 3 --warmup 1
+  python tools/ab_lib.py --variants base tune:17=0 -- --steps 3    (a GK_TUNE_* knob of the base build)
 Prints one JSON object per run and a summary (median it/s, per-projection us).
 """
 import argparse
@@ -28,9 +29,13 @@ def main() -> None:
     for r in range(a.rounds):
         for v in a.variants:
             env = dict(os.environ)
-            if v != "base":
+            tune = []
+            if v.startswith("tune:"):  # a runtime knob of the base build: tune:KEY=VALUE[,KEY=VALUE]
+                for kv in v[5:].split(","):
+                    tune += ["--tune", kv]
+            elif v != "base":
                 env["GK_LIB_DIR"] = os.path.join(ROOT, "gmres_amd", "lib", "variants", v)
-            p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", *extra],
+            p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", *tune, *extra],
                                capture_output=True, text=True, env=env, timeout=a.timeout)
             if p.returncode != 0:
                 print(json.dumps({"variant": v, "round": r, "rc": p.returncode, "err": p.stderr[-800:]}), flush=True)

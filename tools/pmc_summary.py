@@ -50,8 +50,9 @@ def res_fit(a):
              "bytes_per_projection": float(b), "bytes_per_unknown_per_projection": float(b) / n,
              "fit_residual_max_rel": float(np.max(np.abs(y - (b * 2 * js + c)) / y)),
              "per_step": {str(int(j)): float(v) for j, v in zip(js, y)},
-             "per_step_fused_model_ratio": {str(int(j)): float(v / ((32 * j + 16) * n))
+             "per_step_fused_model_ratio": {str(int(j)): float(v / ((32 * j + 16 + (8 if a.sten else 0)) * n))
                                             for j, v in zip(js, y) if j % 16 == 0},
+             "sten": bool(a.sten),
              "source": f"{os.path.relpath(a.fetch)} + {os.path.relpath(a.write)} (every launch j = 1..{a.probe_m} "
                        "of one full cycle, FETCH_SIZE x2 gfx950 correction; L2<->fabric bytes incl. "
                        "Infinity-Cache hits)"}
@@ -75,6 +76,8 @@ def main():
                     help="resident-step kernel (one launch per Arnoldi step j = 1..probe-m in launch order): "
                          "fit bytes per launch = fixed + per_projection * 2j")
     ap.add_argument("--probe-m", type=int, default=95, help="resident launches of the traced cycle (= m)")
+    ap.add_argument("--sten", action="store_true",
+                    help="the step launches formed w = A V(:,j) themselves (gk_res_info sten; model +8n)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
