@@ -398,6 +398,40 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, sten: b
     return roof
 
 
+def rhs_ones_host(N: int, line0: int, nlines: int) -> np.ndarray:
+    """b = A*1 on the slab's lines, on the host: 4 minus the neighbours present."""
+    i = np.arange(N)
+    j = np.arange(line0, line0 + nlines)[:, None]
+    b = 4.0 - (i > 0) - (i < N - 1) - (j > 0).astype(float) - (j < N - 1).astype(float)
+    return np.ascontiguousarray(b.reshape(-1))
+
+
+def pcie_inclusive(ctx, args, run, dist, line0: int, nlines: int, cycles: int = 2) -> dict:
+    """After the timed region: the drop-in's host-buffer flow -- b uploaded from
+    host memory, `cycles` restart cycles, x downloaded into host memory (the
+    solve's own final gk_get_x) -- timed as one, max over ranks.  Not `value`."""
+    import torch
+
+    bh = rhs_ones_host(args.grid, line0, nlines)
+    ctx.sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ctx.set_rhs(bh)
+    r = run(cycles)
+    ctx.sync()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    iters = (r.n_cycles - 1) * args.m + r.n_out
+    return {"cycles": r.n_cycles, "it_s": round(iters / el, 3), "wall_ms": round(el * 1e3, 2),
+            "bytes_over_pcie": 16 * args.grid * args.grid,
+            "note": "b host -> device before the cycles, x device -> host after (the Fortran drop-in's interface); "
+                    "value keeps b and V resident"}
+
+
 def diagnostics(ctx, args, run, dist, world: int) -> dict:
     """After the timed region (not part of `value`): one more cycle with the
     in-kernel clock split on -- per projection / reflection, the time a
@@ -649,6 +683,8 @@ def main() -> None:
     cycles = res.n_cycles
     iters = (cycles - 1) * m + res.n_out if cycles > 0 else 0
     diag = None if args.no_diag else diagnostics(ctx, args, run, dist, world)
+    if diag is not None:
+        diag["pcie_inclusive"] = pcie_inclusive(ctx, args, run, dist, line0, nlines)
 
     sten = args.method == "mgsr" and ctx.res_info().get("sten", 0) == 1
     roof = roofline_entry(prof, args, ctx.nloc, cycles, world, sten) if rank == 0 else None

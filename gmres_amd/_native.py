@@ -29,6 +29,7 @@ GK_TUNE_VERR_ORDER = 14
 GK_TUNE_HH_FUSE = 15
 GK_TUNE_CHEB_STEN = 16
 GK_TUNE_RES_STEN = 17
+GK_TUNE_SPIN_WAIT = 18
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES, GK_KID_PREC = range(8)
 KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res", "prec"]

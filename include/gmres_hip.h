@@ -329,7 +329,9 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          operator the w-only resident MGS step forms w = A V(:,j) in its prologue
  *                          and takes the first dot with it (no stencil launch; even N) -- measured
  *                          4 % slower at 4096^2: the prologue's loads cannot be kept in flight beside
- *                          the register-resident w */
+ *                          the register-resident w
+ *   GK_TUNE_SPIN_WAIT      1 (default): gk_mgs_step_wait / gk_hh_step_wait spin on the step's
+ *                          event; 0: hipEventSynchronize (may sleep in the driver per step) */
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
@@ -348,6 +350,7 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_HH_FUSE 15
 #define GK_TUNE_CHEB_STEN 16
 #define GK_TUNE_RES_STEN 17
+#define GK_TUNE_SPIN_WAIT 18
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

@@ -131,3 +131,20 @@ def test_launcher_never_touches_hip():
 def test_visible_gpus_respects_visibility_env(monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
     assert bench.visible_gpus() == 0
+
+
+def test_host_rhs_matches_the_oracle_on_slabs():
+    """bench.py's PCIe-inclusive leg uploads b = A*1 built on the host: equal to
+    the oracle's manufactured RHS on every row-block slab."""
+    import numpy as np
+
+    from oracle import oracle as orc
+
+    import gmres_amd as ga
+
+    N = 37
+    ref = orc.rhs_ones(N)
+    for R in (1, 3):
+        parts = ga.slab_partition(N, R)
+        b = np.concatenate([bench.rhs_ones_host(N, l0, nl) for l0, nl in parts])
+        assert np.array_equal(b, ref)
