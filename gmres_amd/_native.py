@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import re
 
 PKG = os.path.dirname(os.path.abspath(__file__))
@@ -128,10 +129,27 @@ _FSIGS = {
 }
 
 
+def _one_hip_runtime() -> None:
+    """torch bundles its own libamdhip64 / libhsa-runtime64 / librccl and loads
+    them by path.  Loaded after this library (which links /opt/rocm's), they
+    would be a second HIP runtime in the process -- measured: the process
+    aborts at exit (double free).  Loaded first, their sonames satisfy this
+    library's and the process has one runtime.  So torch, when installed, is
+    imported before the first native load (it is device plumbing for the
+    harness and the tests; the product itself does not use it)."""
+    if "torch" in sys.modules:
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load(path: str, what: str) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise GkError(f"{what} not built at {path}: run `python -m gmres_amd.build` "
                       "(or __graft_entry__.build()); there is no CPU fallback")
+    _one_hip_runtime()
     return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 
 

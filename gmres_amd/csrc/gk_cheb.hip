@@ -321,6 +321,13 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
             tf1 = f0 + nf * CF_U;
         }
         for (int tb = tb0; tb < tf0; tb += CF_U) trip(F{}, tb, tf0);
+        // Drain once before the FAST loop: its header is the first use of the
+        // ring slot loaded D steps earlier, and entering from the prologue with
+        // that slot's load the most recent one made the compiler wait for ALL
+        // loads there on every trip (vmcnt(0) once per 6 steps: the ring's
+        // prefetch lost); with nothing outstanding on entry only the loop's own
+        // back edge counts and the header waits for the one slot it needs.
+        __builtin_amdgcn_s_waitcnt(0);
         for (int tb = tf0; tb < tf1; tb += CF_U) trip(T{}, tb, tf1);
         for (int tb = tf1; tb < tend; tb += CF_U) trip(F{}, tb, tend);
     }
