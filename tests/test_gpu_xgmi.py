@@ -83,8 +83,13 @@ def _check_against_single(ref, res, method):
         assert np.array_equal(res[0].hist_res, r.hist_res)
     k = min(len(ref.hist_res), len(res[0].hist_res))
     h, rr = res[0].hist_res[:k], ref.hist_res[:k]
-    # MGS-R: 1e-3 below r = 1e-6; Householder: the tiers of test_gpu_solver._hist_close_hh
-    tol = np.where(rr > 1e-6, 1e-9, 1e-3 if method == "mgsr" else np.where(rr > 1e-12, 1e-3, 5e-2))
+    # Relative tiers set from the measured drift (tools/multirank_dev.py,
+    # profiles/r03/multirank_dev_r03o.jsonl; 2 and 3 ranks): r > 1e-6 at most
+    # 2.6e-12; MGS-R in (1e-10, 1e-6] at most 1.1e-7, below 1e-10 at most 4.2e-3
+    # (there the 1e-16 absolute term decides).  Householder below 1e-6: the tiers
+    # of test_gpu_solver._hist_close_hh.
+    mg = np.where(rr > 1e-10, 1e-5, 1e-3)
+    tol = np.where(rr > 1e-6, 1e-9, mg if method == "mgsr" else np.where(rr > 1e-12, 1e-3, 5e-2))
     assert np.all(np.abs(h - rr) <= tol * rr + 1e-16), (h, rr)
     x = np.concatenate([r.x for r in res])
     if ref.hist_res[-1] > 1e-6:
