@@ -123,9 +123,9 @@ _FSIGS = {
     "pcg_hip_run": (c_int, [c_vp, c_double, _ip, _dp, c_int, _dp]),
     "pbicgstab_hip_run": (c_int, [c_vp, c_double, _ip, _dp, c_int, _dp]),
     "gmres_mgsr_hip_run": (c_int, [c_vp, c_int, c_double, c_int, c_int, _dp, _dp, _dp, _ip, _ip, c_int, c_int,
-                                   _dp, _dp, _ip]),
+                                   _dp, _dp, _ip, c_int]),
     "gmres_hh_hip_run": (c_int, [c_vp, c_int, c_double, c_int, c_int, c_int, _dp, _dp, _dp, _ip, _ip, c_int,
-                                 c_int, _dp, _dp, _ip]),
+                                 c_int, _dp, _dp, _ip, c_int]),
 }
 
 

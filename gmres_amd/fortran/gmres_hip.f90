@@ -330,7 +330,8 @@ contains
     !> hist_res(c) = true residual after cycle c, hist_ferr(j,c) = final_err(j)
     !> of cycle c (written only when want_hist).  Returns a GK status.
     integer function mgsr_drive(ctx, m, tol, beta0, variant, max_cyc, x, final_err, v_err, n_out, &
-                                restart_out, want_verr, want_hist, hist_res, hist_ferr, n_cycles) result(st)
+                                restart_out, want_verr, want_hist, hist_res, hist_ferr, n_cycles, keep_x) &
+        result(st)
         type(c_ptr), intent(in) :: ctx
         integer, intent(in) :: m, variant, max_cyc
         real(8), intent(in) :: tol, beta0
@@ -338,6 +339,7 @@ contains
         integer, intent(out) :: n_out, restart_out, n_cycles
         logical, intent(in) :: want_verr, want_hist
         real(8), intent(inout) :: hist_res(*), hist_ferr(m, *)
+        logical, intent(in), optional :: keep_x  ! .true.: x stays in HBM (gk_get_x later)
         real(8), allocatable :: H(:, :), g(:), y(:), cs(:), sn(:), hcol(:)
         real(8) :: beta, h_val
         integer :: cyc, j, zero_last
@@ -396,6 +398,9 @@ contains
             zero_last = merge(1, 0, exited)
             st = gk_mgs_verr(ctx, n_out, zero_last, v_err); if (st /= GK_OK) return
         end if
+        if (present(keep_x)) then
+            if (keep_x) return
+        end if
         st = gk_get_x(ctx, x)
     end function mgsr_drive
 
@@ -405,7 +410,7 @@ contains
     !> (:388-566, `converged` latch).
     integer function hh_drive(ctx, m, tol, beta0, precondition, midcycle_exit, max_cyc, x, final_err, &
                               v_err, n_out, stages_out, want_verr, want_hist, hist_res, hist_ferr, &
-                              n_cycles) result(st)
+                              n_cycles, keep_x) result(st)
         type(c_ptr), intent(in) :: ctx
         integer, intent(in) :: m, max_cyc, precondition
         logical, intent(in) :: midcycle_exit
@@ -414,6 +419,7 @@ contains
         integer, intent(out) :: n_out, stages_out, n_cycles
         logical, intent(in) :: want_verr, want_hist
         real(8), intent(inout) :: hist_res(*), hist_ferr(m, *)
+        logical, intent(in), optional :: keep_x  ! .true.: x stays in HBM (gk_get_x later)
         real(8), allocatable :: H(:, :), g(:), y(:), cs(:), sn(:), hcol(:)
         real(8) :: g1
         integer :: k, j
@@ -458,6 +464,9 @@ contains
         end do
         if (want_verr) then
             st = gk_hh_verr(ctx, n_out, v_err); if (st /= GK_OK) return
+        end if
+        if (present(keep_x)) then
+            if (keep_x) return
         end if
         st = gk_get_x(ctx, x)
     end function hh_drive
@@ -809,18 +818,20 @@ end module gmres_hip
 
 ! ----------------------------------------------------------------------------
 ! bind(C) drivers for a harness that already holds a device context (the
-! Python bench / tests, or any C/C++ host).  Arrays are the local slab.
+! Python bench / tests, or any C/C++ host).  Arrays are the local slab;
+! keep_x /= 0 leaves the solution in HBM (x is not written: read it later with
+! gk_get_x), so a timed solve moves nothing over PCIe.
 ! ----------------------------------------------------------------------------
 
 integer(c_int) function gmres_mgsr_hip_run(ctx, m, tol, variant, max_cyc, x, final_err, v_err, n_out, &
-                                           restart_out, want_verr, want_hist, hist_res, hist_ferr, n_cycles) &
-    bind(C, name='gmres_mgsr_hip_run')
+                                           restart_out, want_verr, want_hist, hist_res, hist_ferr, n_cycles, &
+                                           keep_x) bind(C, name='gmres_mgsr_hip_run')
     use, intrinsic :: iso_c_binding
     use gmres_hip_c
     use gmres_hip, only: mgsr_drive
     implicit none
     type(c_ptr), value :: ctx
-    integer(c_int), value :: m, variant, max_cyc, want_verr, want_hist
+    integer(c_int), value :: m, variant, max_cyc, want_verr, want_hist, keep_x
     real(c_double), value :: tol
     real(c_double), intent(out) :: x(*), final_err(*), v_err(*)
     real(c_double), intent(inout) :: hist_res(*), hist_ferr(*)
@@ -830,19 +841,19 @@ integer(c_int) function gmres_mgsr_hip_run(ctx, m, tol, variant, max_cyc, x, fin
     gmres_mgsr_hip_run = gk_rhs_norm(ctx, beta0)
     if (gmres_mgsr_hip_run /= GK_OK) return
     gmres_mgsr_hip_run = mgsr_drive(ctx, int(m), tol, beta0, int(variant), int(max_cyc), x, final_err, v_err, &
-                                    no, ro, want_verr /= 0, want_hist /= 0, hist_res, hist_ferr, nc)
+                                    no, ro, want_verr /= 0, want_hist /= 0, hist_res, hist_ferr, nc, keep_x /= 0)
     n_out = no; restart_out = ro; n_cycles = nc
 end function gmres_mgsr_hip_run
 
 integer(c_int) function gmres_hh_hip_run(ctx, m, tol, precondition, midcycle_exit, max_cyc, x, final_err, &
                                          v_err, n_out, stages_out, want_verr, want_hist, hist_res, hist_ferr, &
-                                         n_cycles) bind(C, name='gmres_hh_hip_run')
+                                         n_cycles, keep_x) bind(C, name='gmres_hh_hip_run')
     use, intrinsic :: iso_c_binding
     use gmres_hip_c
     use gmres_hip, only: hh_drive
     implicit none
     type(c_ptr), value :: ctx
-    integer(c_int), value :: m, precondition, midcycle_exit, max_cyc, want_verr, want_hist
+    integer(c_int), value :: m, precondition, midcycle_exit, max_cyc, want_verr, want_hist, keep_x
     real(c_double), value :: tol
     real(c_double), intent(out) :: x(*), final_err(*), v_err(*)
     real(c_double), intent(inout) :: hist_res(*), hist_ferr(*)
@@ -853,7 +864,7 @@ integer(c_int) function gmres_hh_hip_run(ctx, m, tol, precondition, midcycle_exi
     if (gmres_hh_hip_run /= GK_OK) return
     gmres_hh_hip_run = hh_drive(ctx, int(m), tol, beta0, int(precondition), midcycle_exit /= 0, int(max_cyc), &
                                 x, final_err, v_err, no, so, want_verr /= 0, want_hist /= 0, hist_res, &
-                                hist_ferr, nc)
+                                hist_ferr, nc, keep_x /= 0)
     n_out = no; stages_out = so; n_cycles = nc
 end function gmres_hh_hip_run
 

@@ -345,20 +345,21 @@ def _alloc_hist(m: int, max_cycles: int, want_hist: bool):
 
 
 def gmres_mgsr(ctx: Context, tol: float = 1e-15, variant: int = MGSR_OMP, max_cycles: int = 1000,
-               want_verr: bool = True, want_hist: bool = False) -> SolveResult:
+               want_verr: bool = True, want_hist: bool = False, want_x: bool = True) -> SolveResult:
     """Restarted MGS-R GMRES(m) from x0 = 0 (Fortran host loop, HIP vector work).
-    variant MGSR_OMP = gmres_mgsr_omp semantics, MGSR_MF = gmres_mgsr_mf."""
+    variant MGSR_OMP = gmres_mgsr_omp semantics, MGSR_MF = gmres_mgsr_mf.
+    want_x = False: the solution stays in HBM (result x empty; ctx.get_x() later)."""
     m = ctx.m
-    x = np.zeros(ctx.nloc)
+    x = np.zeros(ctx.nloc if want_x else 1)
     fe = np.zeros(m)
     ve = np.zeros(m + 1)
     n_out, ro, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     hr, hf = _alloc_hist(m, max_cycles, want_hist)
     st = nat.fhost().gmres_mgsr_hip_run(ctx.handle, m, tol, variant, max_cycles, _p(x), _p(fe), _p(ve),
                                         ctypes.byref(n_out), ctypes.byref(ro), int(want_verr), int(want_hist),
-                                        _p(hr), _p(hf), ctypes.byref(nc))
+                                        _p(hr), _p(hf), ctypes.byref(nc), int(not want_x))
     nat.check(st, "gmres_mgsr_hip_run")
-    r = SolveResult(x=x, final_err=fe, v_err=ve, n_out=n_out.value, cycles_out=ro.value, n_cycles=nc.value, m=m)
+    r = SolveResult(x=x if want_x else np.zeros(0), final_err=fe, v_err=ve, n_out=n_out.value, cycles_out=ro.value, n_cycles=nc.value, m=m)
     if want_hist:
         r.hist_res = hr[: nc.value].copy()
         r.hist_ferr = hf.reshape(max_cycles, m)[: nc.value].copy()
@@ -366,22 +367,25 @@ def gmres_mgsr(ctx: Context, tol: float = 1e-15, variant: int = MGSR_OMP, max_cy
 
 
 def gmres_hh(ctx: Context, tol: float = 1e-15, precondition: bool = False, midcycle_exit: bool | None = None,
-             max_cycles: int = 1000, want_verr: bool = True, want_hist: bool = False) -> SolveResult:
+             max_cycles: int = 1000, want_verr: bool = True, want_hist: bool = False,
+             want_x: bool = True) -> SolveResult:
     """Householder GMRES(m): precondition=False -> gmres_hh_omp (full cycles);
-    precondition=True -> gmres_hh_prec_omp (in-cycle convergence latch)."""
+    precondition=True -> gmres_hh_prec_omp (in-cycle convergence latch).
+    want_x = False: the solution stays in HBM (result x empty; ctx.get_x() later)."""
     if midcycle_exit is None:
         midcycle_exit = precondition
     m = ctx.m
-    x = np.zeros(ctx.nloc)
+    x = np.zeros(ctx.nloc if want_x else 1)
     fe = np.zeros(m)
     ve = np.zeros(m + 1)
     n_out, so, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     hr, hf = _alloc_hist(m, max_cycles, want_hist)
     st = nat.fhost().gmres_hh_hip_run(ctx.handle, m, tol, int(precondition), int(midcycle_exit), max_cycles,
                                       _p(x), _p(fe), _p(ve), ctypes.byref(n_out), ctypes.byref(so),
-                                      int(want_verr), int(want_hist), _p(hr), _p(hf), ctypes.byref(nc))
+                                      int(want_verr), int(want_hist), _p(hr), _p(hf), ctypes.byref(nc),
+                                      int(not want_x))
     nat.check(st, "gmres_hh_hip_run")
-    r = SolveResult(x=x, final_err=fe, v_err=ve, n_out=n_out.value, cycles_out=so.value, n_cycles=nc.value, m=m)
+    r = SolveResult(x=x if want_x else np.zeros(0), final_err=fe, v_err=ve, n_out=n_out.value, cycles_out=so.value, n_cycles=nc.value, m=m)
     if want_hist:
         r.hist_res = hr[: nc.value].copy()
         r.hist_ferr = hf.reshape(max_cycles, m)[: nc.value].copy()

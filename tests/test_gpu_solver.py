@@ -255,6 +255,27 @@ def test_true_residual_and_solution(oracle):
         assert ctx.true_residual() == pytest.approx(r.hist_res[-1], rel=1e-12)
 
 
+@pytest.mark.parametrize("method", ["mgsr", "hh"])
+def test_solution_kept_in_hbm(method):
+    """want_x = False (the bench's timed solve): the host x is not written and
+    the device x read afterwards is the one a downloading solve returns."""
+    import gmres_amd as ga
+
+    N, m = 64, 12
+    out = []
+    for want_x in (True, False):
+        with ga.Context(N, m) as ctx:
+            ctx.set_rhs_ones()
+            if method == "mgsr":
+                r = ga.gmres_mgsr(ctx, 1e-15, max_cycles=3, want_verr=False, want_x=want_x)
+            else:
+                r = ga.gmres_hh(ctx, 1e-15, max_cycles=3, want_verr=False, want_x=want_x)
+            assert r.x.size == (N * N if want_x else 0)
+            out.append((r.x if want_x else ctx.get_x(), r.n_cycles, r.n_out))
+    assert out[0][1:] == out[1][1:]
+    assert np.array_equal(out[0][0], out[1][0])
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("prec,key", [("identity", "mgsr_identity_4096_m95"), ("cbpr2", "mgsr_cbpr2_4096_m95")])
 def test_4096_first_cycle_vs_reference(prec, key):

@@ -28,6 +28,7 @@ def main() -> None:
     ap.add_argument("--prof", type=int, default=0, help="HIP events every S-th step in the timed cycles (bench: 16)")
     ap.add_argument("--hist-warm", action="store_true", help="warmup cycle with the per-cycle true residual")
     ap.add_argument("--method", default="mgsr", choices=["mgsr", "hh"])
+    ap.add_argument("--keep-x", action="store_true", help="timed solve leaves x in HBM (no final download)")
     a = ap.parse_args()
     import torch
 
@@ -46,11 +47,11 @@ def main() -> None:
             c.set_precond(prec, (8.2, 0.2), deg)
             c.set_rhs_ones()
 
-            def run(k, hist=False):
+            def run(k, hist=False, want_x=True):
                 if a.method == "mgsr":
-                    return ga.gmres_mgsr(c, 1e-15, max_cycles=k, want_verr=False, want_hist=hist)
+                    return ga.gmres_mgsr(c, 1e-15, max_cycles=k, want_verr=False, want_hist=hist, want_x=want_x)
                 return ga.gmres_hh(c, 1e-15, precondition=prec != "identity", max_cycles=k, want_verr=False,
-                                   want_hist=hist)
+                                   want_hist=hist, want_x=want_x)
 
             run(1, a.hist_warm)
             if a.prof:
@@ -58,12 +59,12 @@ def main() -> None:
                 c.profile_reset()
             c.sync()
             t0 = time.perf_counter()
-            r = run(a.cycles)
+            r = run(a.cycles, want_x=not a.keep_x)
             c.sync()
             t1 = time.perf_counter()
         iters = (r.n_cycles - 1) * 95 + r.n_out
         print(json.dumps({"leg": i, "prec": prec, "grid": a.grid, "method": a.method, "prof": a.prof,
-                          "hist_warm": a.hist_warm, "pre_grid": a.pre_grid, "ms_per_cycle": round((t1 - t0) / r.n_cycles * 1e3, 3),
+                          "hist_warm": a.hist_warm, "pre_grid": a.pre_grid, "keep_x": a.keep_x, "ms_per_cycle": round((t1 - t0) / r.n_cycles * 1e3, 3),
                           "it_s": round(iters / (t1 - t0), 3)}), flush=True)
 
 
