@@ -605,16 +605,35 @@ def main() -> None:
         ctx.tune(10, world)  # GK_TUNE_RES_SHARE
     ml = max(p[1] for p in parts)
     collective = None
+    rccl_failed = None  # RCCL init failed on some rank; the device exchange carries every collective
     if world > 1 and args.collective == "xgmi":
         ctx.comm_init_xgmi(world, rank, ml)
     elif world > 1 or os.environ.get("GK_FORCE_RCCL") == "1":  # 1-rank RCCL: exercises the comm path
         obj = [ga.Context.unique_id() if rank == 0 else None]
         if dist is not None:
             dist.broadcast_object_list(obj, src=0)
-        ctx.comm_init(world, rank, ml, obj[0])
-        collective = "rccl"
+        ok, why = 1, ""
+        try:
+            ctx.comm_init(world, rank, ml, obj[0])
+        except ga.GkError as e:
+            ok, why = 0, str(e)
+            print(f"rank {rank}: RCCL communicator failed: {e}", file=sys.stderr)
+        if dist is not None:
+            t = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = int(t.item())
+        if ok:
+            collective = "rccl"
+        elif world > 1 and args.collective == "auto":
+            # every rank together: the slab decomposition without RCCL, collectives
+            # by the device exchange only (setup_xgmi below must then succeed)
+            rccl_failed = why[:300] or "a peer rank's RCCL init failed"
+            ctx.comm_init_xgmi(world, rank, ml)
+        else:
+            raise RuntimeError(f"RCCL communicator: {why or 'a peer rank failed'}")
     if world > 1 and args.collective in ("auto", "xgmi"):
-        collective = setup_xgmi(ctx, dist, world, rank, required=args.collective == "xgmi") or "rccl"
+        collective = setup_xgmi(ctx, dist, world, rank,
+                                required=args.collective == "xgmi" or rccl_failed is not None) or "rccl"
     for kv in args.tune:
         k, v = kv.split("=")
         ctx.tune(int(k), int(v))
@@ -724,6 +743,7 @@ def main() -> None:
                        "grid": N, "m": m, "precond": args.prec, "method": args.method,
                        "step": "one GMRES(m) restart cycle", "parallelism": f"row-block slabs x{world}",
                        "collective": collective, "comm_ranks_seen": comm["nranks"], "comm_kind": comm["kind"],
+                       "rccl_init_failed": rccl_failed,
                        "arnoldi_iters": iters},
             "fallback": fallback,
             "check": check,

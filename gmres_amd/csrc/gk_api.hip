@@ -1412,7 +1412,9 @@ int gk_comm_init(gk_ctx *c, int nranks, int rank, int max_lines, const unsigned 
     if (nranks > 1 || (force != nullptr && force[0] == '1')) {
         ncclUniqueId u;
         std::memcpy(&u, id, 128);
-        NCCLCHK(ncclCommInitRank(&c->comm, nranks, u, rank));
+        ncclComm_t cm = nullptr;  // c->comm stays null when the init fails (gk_destroy, a later
+        NCCLCHK(ncclCommInitRank(&cm, nranks, u, rank));  // gk_comm_init_xgmi)
+        c->comm = cm;
         c->comm_ok = true;
     }
     return GK_OK;
