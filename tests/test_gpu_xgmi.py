@@ -360,3 +360,30 @@ def test_straggling_process_is_named_within_the_deadline():
     # the device is healthy: a fresh solve converges as before
     r = _single(32, 10, "mgsr", "identity", 1, 100)
     assert r.hist_res[-1] < 1e-12
+
+
+# ------------------------------------------- the driver's N-rank bench line ---
+
+def test_bench_two_ranks_default_collective_on_one_gpu():
+    """bench.py --gpus 2 as the driver runs it (its own torch.distributed
+    launch, the default --collective auto), both ranks on this GPU
+    (GK_BENCH_SAME_DEVICE): RCCL refuses two ranks on one device, so every rank
+    falls back together to the device exchange alone, and the line's cycle-1
+    residual still matches the reference's own 1024^2 run."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GK_BENCH_SAME_DEVICE="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--grid", "1024",
+                        "--steps", "1", "--warmup", "1", "--no-cpu", "--no-diag"],
+                       capture_output=True, text=True, env=env, cwd=root, timeout=100)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["fallback"] is None
+    assert line["config"]["collective"] == "xgmi-device-exchange"
+    assert line["config"]["comm_ranks_seen"] == 2
+    assert line["check"]["pass"], line["check"]
