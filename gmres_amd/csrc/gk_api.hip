@@ -1463,6 +1463,11 @@ int gk_comm_init_xgmi(gk_ctx *c, int nranks, int rank, int max_lines) {
     if (c == nullptr || nranks < 1 || nranks > gk::XS_MAXR || rank < 0 || rank >= nranks || max_lines < c->nlines)
         return set_err(GK_ERR_ARG, "bad xgmi comm args (nranks <= %d)", gk::XS_MAXR);
     HIPCHK(hipSetDevice(c->dev));
+    if (c->comm != nullptr) {  // an RCCL communicator of an abandoned gk_comm_init: the exchange replaces it
+        ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+        c->comm_ok = false;
+    }
     c->nranks = nranks;
     c->rank = rank;
     c->max_lines = max_lines;
