@@ -19,8 +19,10 @@ refuses (exit 2) when fewer than N GPUs are visible.  --plan-only prints that
 launch plan as JSON and exits.  The grid is split into row-block slabs of grid
 lines (strong scaling: the global grid is fixed as N grows); per projection
 the dot products are all-reduced inside libgmres_hip (device exchange over
-xGMI, or RCCL), halo lines exchanged point to point; torch.distributed (gloo)
-only bootstraps the communicator and times max-over-ranks.
+xGMI, or RCCL), halo lines exchanged point to point; a small TCP control
+plane on the loopback interface (gmres_amd/ctl.py) only bootstraps the
+communicator and times max-over-ranks.  No rank imports torch: the library
+runs on the HIP runtime and RCCL it was built against (config.runtime).
 
 Rank 0 prints ONE JSON line.
 """
@@ -64,27 +66,68 @@ def mgs_step_bytes(n: int, j: int, model: str, sten: bool = False) -> float:
     return float((32 * j + 16 + (8 if sten else 0)) * n)
 
 
+def res_regions(plan: dict, nloc: int) -> dict:
+    """How a resident launch holds the slab (gk_res_info): unknowns whose w AND
+    running Krylov column sit in registers ("pairs": the pairs / prefetch
+    variants), unknowns whose w alone is on chip (registers of the w-only
+    variant, or LDS), and the streamed rest.  Chunks of DT double2: 256 (w-only),
+    448 (prefetch, one control wave), 512 (pairs)."""
+    n2 = nloc // 2
+    dt = 256 if plan["variant"] == "w-only" else (448 if plan.get("cw") else 512)
+    nres2 = min(int(plan["nres2"]), n2)
+    nreg2 = min(nres2, int(plan["G"]) * int(plan["r2e"]) * dt)
+    if plan["variant"] == "w-only":
+        return {"pairs": 0, "w_on_chip": 2 * nres2, "streamed": 2 * (n2 - nres2) + (nloc & 1)}
+    return {"pairs": 2 * nreg2, "w_on_chip": 2 * (nres2 - nreg2), "streamed": 2 * (n2 - nres2) + (nloc & 1)}
+
+
+def res_launch_bytes(plan: dict, nloc: int, P: int, mgs: bool = True, sten: bool = False) -> float:
+    """Compulsory bytes of ONE resident launch of the selected variant running P
+    passes (an MGS-R step: P = 2j, the last one closing with ||w||; a Householder
+    chain: P = L reflections), per unknown of each region (res_regions):
+      pairs       w in 8, one Krylov column per pass (the AXPY partner of pass
+                  p+1 is pass p's dot partner, still in registers): 8P, out 8
+                  -> 8P + 16
+      w on chip   w in 8, both columns of every pass but the last (no dot
+                  partner) 16P - 8, out 8 -> 16P + 8
+      streamed    w read + written, both columns, every pass: 32P - 8; the MGS
+                  step then reads w once more and writes V(:,j+1): +16
+    sten: the launch forms w = A V(:,j) itself (reads V(:,j) and V(:,1) instead
+    of w: +8 per resident unknown)."""
+    r = res_regions(plan, nloc)
+    b = r["pairs"] * (8 * P + 16) + r["w_on_chip"] * (16 * P + 8) + r["streamed"] * (32 * P - 8 + (16 if mgs else 0))
+    if sten:
+        b += 8 * (r["pairs"] + r["w_on_chip"])
+    return float(b)
+
+
 def hh_chain_bytes(n: int, L: int, model: str) -> float:
     """One resident Householder chain of L reflections w -= 2<w,P_i>P_i."""
     return float(40 * L * n if model == "as_written" else (16 * L + 16) * n)
 
 
-def prec_bytes(n: int, prec: str, degree: int, model: str) -> float:
-    """One preconditioner application after the stencil (z = A v already made)."""
+def prec_bytes(n: int, prec: str, degree: int, model: str, cheb_sten: bool = True) -> float:
+    """One preconditioner application after the stencil (z = A v already made).
+    cheb_sten: the Arnoldi step's Chebyshev pass forms z = A v in its own stage
+    0 (gk_res_info "cheb_sten"; off with GK_TUNE_CHEB_STEN 0, N < 128, k > 8,
+    or a slab thinner than k + 1 lines)."""
     if prec == "identity":
         return 0.0
     if prec == "cbpr2":
         return float(64 * n if model == "as_written" else 16 * n)
     # Chebyshev(k): 48n per sweep as written; fused, k <= 8 sweeps are ONE
-    # temporal-blocked pass whose stage 0 is the stencil itself (reads v, writes
-    # the result, reads the dot partner: the 24n the stencil term already
-    # counts, so +0); each further pass of up to 8 hands over (d, r, z): +48n
-    # (and the first pass then runs after a stencil launch: +16n)
+    # temporal-blocked pass.  With the stencil as its stage 0 it reads v, writes
+    # the result and reads the dot partner -- the 24n the stencil term already
+    # counts, so +0; after a stencil launch it reads z and writes the result
+    # (+16n).  Each further pass of up to 8 hands over (d, r, z): +48n.
     passes = (degree + 7) // 8
-    return float(48 * degree * n if model == "as_written" else (0 if passes == 1 else 16 + 48 * (passes - 1)) * n)
+    if model == "as_written":
+        return float(48 * degree * n)
+    return float(((0 if (passes == 1 and cheb_sten) else 16) + 48 * (passes - 1)) * n)
 
 
-def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str, sten: bool = False) -> float:
+def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str, sten: bool = False,
+                cheb_sten: bool = True) -> float:
     """One full restart cycle of m Arnoldi steps (sten: the step launches form
     w = A V(:,j) themselves -- the stencil's 24n become the launch's +8n)."""
     if model == "as_written":  # SURVEY 8(d): per step (40 + 80 j) n, cycle start 64n, update 8(m+2)n
@@ -100,7 +143,8 @@ def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str,
     else:
         b = sum(mgs_step_bytes(n, j, model, sten) + (0 if sten else st) for j in range(1, m + 1))
         b += 40 * n + 8 * (m + 2) * n  # cycle start (b - A x, norm, V_1) + x update
-    return float(b + (m + 1) * prec_bytes(n, prec, degree, model))
+    # the cycle start's application runs after a stencil launch (never stage-0 fused)
+    return float(b + m * prec_bytes(n, prec, degree, model, cheb_sten) + prec_bytes(n, prec, degree, model, False))
 
 
 # ------------------------------------------------------------- CPU baseline ---
@@ -152,17 +196,19 @@ def sweep_threads(share: int) -> list[int]:
     return ts + [share]
 
 
-def cpu_baseline(N: int, m: int, prec: str, degree: int, method: str, cap_full: float, cap_leg: float) -> dict:
+def cpu_baseline(N: int, m: int, prec: str, degree: int, method: str, cap_full: float, steps: int) -> dict:
     """The reference CPU path timed on this host (rank 0, N = 1 only):
     oracle/_ref/ref_driver = the reference's own gmres_mgsr_omp / gmres_hh_omp
     (kind "reference"); Chebyshev(k) does not exist in the reference, so that
     config times the restatement (kind "port").  Thread sweep in the
     reference's own strong-scaling pattern (1, 2, 4, 8, 16 threads, capped at
-    the process's OpenMP share; OMP_PROC_BIND=close, OMP_PLACES=cores): every
-    leg below the share runs a bounded sample of cycle 1 (the first steps
-    within cap_leg seconds, step cost fitted a + b j and summed over the cycle);
-    the share itself runs one full cycle when it finishes within cap_full
-    seconds (else a fitted sample).  `value` is the fastest leg."""
+    the process's OpenMP share; OMP_PROC_BIND=close, OMP_PLACES=cores).  Every
+    leg, the share included, times the SAME window -- Arnoldi steps 1..`steps`
+    of cycle 1 from x0 = 0, stamped by omp_get_wtime -- and prices the cycle
+    identically: step cost fitted a + b j over steps 2..`steps` (step 1 pays the
+    solve's first touches), summed over j = 1..m.  `value` is the fastest leg.
+    The share also runs one full cycle when it fits cap_full seconds: a check
+    of the fit (`full_cycle_check`), not the value."""
     from oracle import refrun
 
     info = cpu_info()
@@ -171,39 +217,46 @@ def cpu_baseline(N: int, m: int, prec: str, degree: int, method: str, cap_full: 
     use_ref = refrun.available() and prec in ("identity", "cbpr2")
     solver = ("hh_omp" if prec == "identity" else "hh_prec_omp") if method == "hh" else "mgsr_omp"
     share = info["omp_threads"]
-    for thr in sweep_threads(share):
-        cap = cap_full if thr == share else cap_leg
-        t0 = time.perf_counter()
-        if use_ref:
-            e = dict(env, REF_TIME_CAP=str(cap))
-            r = refrun.run(solver, N, m, prec, threads=thr, max_cycles=1, env=e, timeout=cap + 600)
-            c0 = r.cycle_t[0]
-            if len(r.cycle_t) >= 2:  # full cycle: stamps at the starts of cycles 1 and 2
-                t_cyc, how = r.cycle_t[1] - c0, "one full cycle timed (omp_get_wtime stamps of cycles 1 and 2)"
-            else:
-                t_cyc, how = _extrapolate(r.step_t, c0, m)
-            thr_used = r.threads
-        else:
-            from oracle import oracle as orc
 
-            kind = {"identity": orc.PREC_IDENTITY, "cbpr2": orc.PREC_CBPR2, "cheb": orc.PREC_CHEB}[prec]
-            steps = m if thr == share else 12
-            rr = orc.gmres_mgsr(orc.rhs_ones(N), N, m, prec=kind, degree=degree, variant=orc.MGSR_OMP,
-                                max_cycles=1, step_limit=steps, threads=thr)
-            st = {j + 1: float(t) for j, t in enumerate(rr.step_times) if t > 0}
-            t_cyc, how = _extrapolate(st, 0.0, m)
-            thr_used = thr
+    def leg(thr: int, step_limit: int):
+        if use_ref:
+            r = refrun.run(solver, N, m, prec, threads=thr, max_cycles=1, step_limit=step_limit, env=env,
+                           timeout=900)
+            return r.step_t, r.cycle_t, r.threads
+        from oracle import oracle as orc
+
+        kind = {"identity": orc.PREC_IDENTITY, "cbpr2": orc.PREC_CBPR2, "cheb": orc.PREC_CHEB}[prec]
+        rr = orc.gmres_mgsr(orc.rhs_ones(N), N, m, prec=kind, degree=degree, variant=orc.MGSR_OMP,
+                            max_cycles=1, step_limit=step_limit or m, threads=thr)
+        st = {j + 1: float(t) for j, t in enumerate(rr.step_times) if t > 0}
+        return st, [0.0], thr
+
+    for thr in sweep_threads(share):
+        t0 = time.perf_counter()
+        step_t, cycle_t, thr_used = leg(thr, steps)
+        t_cyc, how = _extrapolate(step_t, cycle_t[0], m)
         legs.append({"threads": thr_used, "cycle_s": round(t_cyc, 3), "it_s": round(m / t_cyc, 4), "how": how,
                      "wall_s": round(time.perf_counter() - t0, 1)})
     best = max(legs, key=lambda d: d["it_s"])
+    check = None
+    if use_ref and cap_full > 0 and legs[-1]["cycle_s"] <= cap_full:
+        t0 = time.perf_counter()
+        r = refrun.run(solver, N, m, prec, threads=share, max_cycles=1, env=env, timeout=cap_full + 600)
+        if len(r.cycle_t) >= 2:
+            full = r.cycle_t[1] - r.cycle_t[0]
+            check = {"threads": r.threads, "cycle_s": round(full, 3), "it_s": round(m / full, 4),
+                     "fit_over_full": round(legs[-1]["cycle_s"] / full, 4),
+                     "how": "one full cycle (omp_get_wtime stamps of cycles 1 and 2)",
+                     "wall_s": round(time.perf_counter() - t0, 1)}
     return {"value": best["it_s"], "unit": "Arnoldi it/s", "cores": best["threads"],
             "kind": "reference" if use_ref else "port",
             "sample": (f"{'oracle/_ref/ref_driver (the reference src/*.f90 built by oracle/Makefile.ref)' if use_ref else 'oracle/gmres_oracle.c (restatement; Chebyshev(k) is not in the reference)'} "
                        f"{solver} on {N}^2 m={m} prec={prec}, b = A*1, x0 = 0; thread sweep "
                        f"{[d['threads'] for d in legs]} (the reference's strong-scaling pattern, capped at the "
-                       f"process's OpenMP share of {share}); value = the fastest leg ({best['threads']} threads: "
-                       f"{best['how']}); legs below the share: cycle 1 cut after {cap_leg:g} s, a + b j fit"),
-            "sweep": legs,
+                       f"process's OpenMP share of {share}); every leg times Arnoldi steps 1..{steps} of cycle 1 "
+                       f"and prices the cycle by the same a + b j fit; value = the fastest leg "
+                       f"({best['threads']} threads)"),
+            "sweep": legs, "full_cycle_check": check,
             "hbm_gbps_alg_as_written": round(cycle_bytes(N * N, m, prec, degree, method, "as_written")
                                              / best["cycle_s"] / 1e9, 1),
             "host": info, "calibration": "profiles/r02/cpu_calibration.json"}
@@ -281,17 +334,14 @@ def maybe_self_launch(args, argv: list[str]) -> None:
 
 
 # ------------------------------------------------------------- device exchange
-def setup_xgmi(ctx, dist, world: int, rank: int, required: bool):
-    """Map every rank's exchange region (IPC handles over the gloo control
-    plane) and run the collective self-test; every rank must pass, else all
-    ranks fall back to RCCL (or fail when --collective xgmi was asked for)."""
-    import torch
-
+def setup_xgmi(ctx, ctl, rank: int, required: bool):
+    """Map every rank's exchange region (IPC handles over the control plane,
+    gmres_amd/ctl.py) and run the collective self-test; every rank must pass,
+    else all ranks fall back to RCCL (or fail when --collective xgmi was asked
+    for, or when there is no RCCL communicator to fall back to)."""
     ok = 1
-    hs = [None] * world
     try:
-        h = ctx.xchg_handle()
-        dist.all_gather_object(hs, h)
+        hs = ctl.allgather(ctx.xchg_handle())
         ctx.xchg_open(hs)
     except Exception as e:  # noqa: BLE001 - reported, then the self-test decides
         print(f"rank {rank}: device exchange unavailable: {e}", file=sys.stderr)
@@ -300,23 +350,25 @@ def setup_xgmi(ctx, dist, world: int, rank: int, required: bool):
         ok = int(ctx.xchg_selftest(5000))
         if not ok:
             print(f"rank {rank}: {getattr(ctx, 'xchg_error', '')}", file=sys.stderr)
-    t = torch.tensor([ok], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)
-    if int(t.item()) == 1:
+    if ctl.allreduce(ok, "min") == 1:
         return "xgmi-device-exchange"
     if required:
-        raise RuntimeError("--collective xgmi: device exchange self-test failed")
+        raise RuntimeError("device exchange self-test failed on some rank (and no RCCL fallback: --collective xgmi, "
+                           "or the RCCL communicator failed too)")
     if ok:
         ctx.xchg_enable(False)
     return None
 
 
-def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, sten: bool = False) -> dict | None:
-    """Dominant kernel: its algorithmic bytes per launch (fused-minimum model)
-    over its average launch time from HIP events on the context stream.  sten:
-    the MGS step launch forms w = A V(:,j) itself (gk_res_info "sten")."""
+def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: dict | None = None,
+                   sten: bool = False) -> dict | None:
+    """Dominant kernel: its compulsory bytes per launch over its average launch
+    time from HIP events on the context stream.  `plan` = gk_res_info of the
+    timed context (the resident variant the launches ran: its bytes are
+    res_launch_bytes); sten: the MGS step launch forms w = A V(:,j) itself."""
     m = args.m
-    if not prof or prof.get("res", (0.0, 0))[1] == 0:
+    on_res = bool(prof) and prof.get("res", (0.0, 0))[1] > 0 and plan is not None and plan.get("variant")
+    if not on_res:
         if not prof or prof["proj"][1] == 0:
             return None
         # launch-per-projection path (RCCL multi-rank, or after a fallback)
@@ -328,12 +380,16 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, sten: b
         kname = "gk::k_proj (AXPY_i fused with dot_{i+1}, one launch per projection)"
         timing = f"HIP events around every projection launch of steps j % {S} == 0 of the timed cycles"
         per_proj = ms * 1e3 / launches
+        variant, regions, bound, peak = "launch-per-projection", None, "hbm", HBM_PEAK_GBPS
+        model = "32 B per unknown per projection (w read + written, both Krylov columns)"
     else:
         ms, launches = prof["res"]
+        variant = plan["variant"]
+        regions = res_regions(plan, nloc)
         if args.method == "hh":
             steps_js = list(range(1, m + 1)) * cycles
             chains = [j for j in steps_js for _ in (0, 1)] + [m] * cycles
-            fused = sum(hh_chain_bytes(nloc, L, "fused") for L in chains)
+            fused = sum(res_launch_bytes(plan, nloc, L, mgs=False) for L in chains)
             written = sum(hh_chain_bytes(nloc, L, "as_written") for L in chains)
             nproj = sum(chains)
             kname = ("gk::k_mgs_wres / k_mgs_res in reflection mode (RES_HH_DOWN / RES_HH_UP: a chain of j "
@@ -342,7 +398,7 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, sten: b
         else:
             S = max(1, args.prof_every)
             steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
-            fused = sum(mgs_step_bytes(nloc, j, "fused", sten) for j in steps_js)
+            fused = sum(res_launch_bytes(plan, nloc, 2 * j, mgs=True, sten=sten) for j in steps_js)
             written = sum(mgs_step_bytes(nloc, j, "as_written", sten) for j in steps_js)
             nproj = sum(2 * j for j in steps_js)
             kname = ("gk::k_mgs_wres / k_mgs_res (resident MGS-R step: 2j fused projections + norm + scale, one "
@@ -350,38 +406,53 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, sten: b
                                                              "launch's prologue)" if sten else ")"))
             timing = f"HIP events on the context stream around the step launch of steps j % {S} == 0 of the timed cycles"
         per_proj = ms * 1e3 / nproj
+        model = ("compulsory bytes of the selected resident variant (bench.res_launch_bytes, DESIGN.md §3): per "
+                 "pass 8 B per unknown whose w and running column sit in registers, 16 B per unknown whose w alone "
+                 "is on chip, 32 B per streamed unknown; plus w in and V(:,j+1) out")
+        # Which memory ceiling binds.  The w-only variant reads each pass's dot column
+        # V_q with the default policy so that it is still in the 256 MiB Infinity
+        # Cache when the next pass reads it as V_i: its bytes cross the L2 <-> fabric
+        # boundary (Infinity-Cache hits included), about half of them from DRAM --
+        # the fabric read rate binds.  The other variants load their columns
+        # non-temporally or hold the reused column in registers: every byte is DRAM.
+        if variant == "w-only":
+            bound, peak = "fabric", FABRIC_REF_GBPS
+        else:
+            bound, peak = "hbm", HBM_PEAK_GBPS
     secs = ms / 1e3
     ach = fused / secs / 1e9
-    roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None, "model": "fused minimum (DESIGN.md §3)",
+    roof = {"bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
+            "frac": round(ach / peak, 4), "traffic": None, "model": model, "variant": variant,
+            "regions_unknowns": regions,
+            "hbm_spec_frac": round(ach / HBM_PEAK_GBPS, 4),
             "kernel": kname, "launches": launches, "avg_launch_us": round(ms * 1e3 / launches, 2),
             "alg_bytes_per_launch": round(fused / launches), "per_projection_us": round(per_proj, 2),
             "alg_as_written_bytes_per_launch": round(written / launches),
             "alg_as_written_frac": round(written / secs / 1e9 / HBM_PEAK_GBPS, 4),
             "timing": timing, "per_kernel_ms_sampled": {k: round(v[0], 3) for k, v in prof.items()}}
-    if prof.get("res", (0.0, 0))[1] > 0 and args.method == "mgsr":
-        # Which ceiling binds: the fused bytes cross the L2 <-> Infinity Fabric
-        # boundary, but V_i (the AXPY column) is the previous pass's dot column
-        # V_q, read with the default policy so that it is still in the 256 MiB
-        # Infinity Cache: DRAM sees only the dot column of each pass plus w in and
-        # V(:,j+1) out, (16j + 16) n per step launch.  A/B evidence (V_q
-        # non-temporal, so V_i must come from HBM): 41.07 -> 45.06 us per
-        # projection, 5.96 TB/s of HBM traffic = the achievable HBM rate
-        # (profiles/r03/ab_qnt_r03d.jsonl, MI355X_MICROARCH.md 6.0-6.3 TB/s).
-        dram = sum((16.0 * j + 16.0 + (8.0 if sten else 0.0)) * nloc for j in steps_js)
+    if bound == "fabric":
+        roof["peak_source"] = ("MI355X_MICROARCH.md: Infinity-Cache-resident reads 8.6 TB/s chip-wide (the rate "
+                               "the L2 <-> fabric boundary sustains when lines come from the Infinity Cache)")
+        # DRAM side: each pass's dot column from HBM, its AXPY column from the
+        # Infinity Cache; w in, V(:,j+1) out.  A/B evidence (V_q non-temporal, so V_i
+        # must come from HBM): 41.07 -> 45.06 us per projection, 5.96 TB/s of HBM
+        # traffic = the achievable HBM rate (profiles/r03/ab_qnt_r03d.jsonl).
+        if args.method == "hh":
+            dram = sum((8.0 * L + 16.0) * nloc for L in chains)
+        else:
+            dram = sum((16.0 * j + 16.0 + (8.0 if sten else 0.0)) * nloc for j in steps_js)
         roof["ceiling"] = ("fabric: L2 <-> Infinity Fabric read rate (Infinity-Cache hits included); the DRAM "
-                           "side carries about half of the fused bytes")
-        roof["fabric"] = {"achieved": roof["achieved"], "peak_ref": FABRIC_REF_GBPS,
-                          "frac": round(roof["achieved"] / FABRIC_REF_GBPS, 4),
-                          "peak_source": "MI355X_MICROARCH.md: Infinity-Cache-resident reads 8.6 TB/s chip-wide"}
-        roof["dram"] = {"bytes_per_launch_est": round(dram / launches), "achieved": round(dram / secs / 1e9, 1),
-                        "frac": round(dram / secs / 1e9 / HBM_PEAK_GBPS, 4),
-                        "model": "(16 j + 16) n per step: each pass's dot column from HBM, its AXPY column from the "
-                                 "Infinity Cache; w (or, forming w in the launch, V(:,j) and V(:,1)) in, V(:,j+1) out",
-                        "evidence": "profiles/r03/ab_qnt_r03d.jsonl (V_q non-temporal: +9.7 % per projection)"}
+                           "side carries about half of these bytes")
+        roof["hbm"] = {"bytes_per_launch_est": round(dram / launches), "achieved": round(dram / secs / 1e9, 1),
+                       "peak": HBM_PEAK_GBPS, "frac": round(dram / secs / 1e9 / HBM_PEAK_GBPS, 4),
+                       "model": "each pass's dot column from HBM, its AXPY column from the Infinity Cache; w (or, "
+                                "forming w in the launch, V(:,j) and V(:,1)) in, the output column out",
+                       "evidence": "profiles/r03/ab_qnt_r03d.jsonl (V_q non-temporal: +9.7 % per projection)"}
+    else:
+        roof["ceiling"] = "hbm: every compulsory byte is a DRAM byte (non-temporal column loads / register reuse)"
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    key = f"{args.grid}_{m}_{args.prec}_{args.method}_{world}_res"
-    if os.path.exists(tf) and prof.get("res", (0, 0))[1] > 0 and args.method == "mgsr":
+    if os.path.exists(tf) and on_res and args.method == "mgsr":
+        key = pmc_key(variant, nloc, m, args.prec, args.method)
         pm = json.load(open(tf)).get(key)
         if pm and bool(pm.get("sten", False)) != sten:  # measured on the other step flow: not this kernel's bytes
             pm = None
@@ -391,11 +462,19 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, sten: b
                 tb = sum(per_step[j] for j in steps_js) / len(steps_js)
                 roof["traffic"] = round(tb)
                 roof["traffic_source"] = pm["source"]
+                roof["traffic_key"] = key
                 roof["physical"] = {"fabric_GBps": round(tb * launches / secs / 1e9, 1),
                                     "traffic_over_alg": round(tb * launches / fused, 3),
                                     "note": "FETCH_SIZE (x2, gfx950) + WRITE_SIZE at the same steps j: L2<->fabric "
                                             "bytes, Infinity-Cache hits included"}
     return roof
+
+
+def pmc_key(variant: str, nloc: int, m: int, prec: str, method: str) -> str:
+    """profiles/pmc_traffic.json key of a resident kernel's per-step PMC bytes:
+    the variant and the slab it ran on (the same kernel at the same load gives
+    the same bytes on 1 GPU and on every GPU of an N-rank split)."""
+    return f"res_{variant}_{nloc}_{m}_{prec}_{method}"
 
 
 def rhs_ones_host(N: int, line0: int, nlines: int) -> np.ndarray:
@@ -406,25 +485,18 @@ def rhs_ones_host(N: int, line0: int, nlines: int) -> np.ndarray:
     return np.ascontiguousarray(b.reshape(-1))
 
 
-def pcie_inclusive(ctx, args, run, dist, line0: int, nlines: int, cycles: int = 2) -> dict:
+def pcie_inclusive(ctx, args, run, ctl, line0: int, nlines: int, cycles: int = 2) -> dict:
     """After the timed region: the drop-in's host-buffer flow -- b uploaded from
     host memory, `cycles` restart cycles, x downloaded into host memory (the
     solve's own final gk_get_x) -- timed as one, max over ranks.  Not `value`."""
-    import torch
-
     bh = rhs_ones_host(args.grid, line0, nlines)
     ctx.sync()
-    if dist is not None:
-        dist.barrier()
+    ctl.barrier()
     t0 = time.perf_counter()
     ctx.set_rhs(bh)
     r = run(cycles)
     ctx.sync()
-    el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
+    el = ctl.allreduce(time.perf_counter() - t0, "max")
     iters = (r.n_cycles - 1) * args.m + r.n_out
     return {"cycles": r.n_cycles, "it_s": round(iters / el, 3), "wall_ms": round(el * 1e3, 2),
             "bytes_over_pcie": 16 * args.grid * args.grid,
@@ -432,15 +504,13 @@ def pcie_inclusive(ctx, args, run, dist, line0: int, nlines: int, cycles: int = 
                     "value keeps b, V and x resident (x is read back after the timed region)"}
 
 
-def diagnostics(ctx, args, run, dist, world: int) -> dict:
+def diagnostics(ctx, args, run, ctl, world: int) -> dict:
     """After the timed region (not part of `value`): one more cycle with the
     in-kernel clock split on -- per projection / reflection, the time a
     resident launch spends streaming its pass vs waiting in the in-launch
     all-gather (on N ranks that wait includes the cross-device rank totals) --
     and on N ranks the collective's own latency (gk_comm_latency).  Max over
     ranks, so the 8-GPU line carries the cross-device price beside it."""
-    import torch
-
     m = args.m
     if args.method == "mgsr":
         kinds = [(0, "mgs_step", m * (m + 1))]
@@ -459,10 +529,8 @@ def diagnostics(ctx, args, run, dist, world: int) -> dict:
     if world > 1:
         c = ctx.comm_latency(200)
         lat = [c["allreduce_us"], c["halo_us"]]
-    t = torch.tensor(vals + lat, dtype=torch.float64)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    v = [round(float(x), 3) for x in t.tolist()]
+    allv = ctl.allgather(vals + lat)
+    v = [round(float(max(col)), 3) for col in zip(*allv)]
     split = {}
     for k, (_, name, _) in enumerate(kinds):
         if v[2 * k] >= 0:
@@ -479,23 +547,41 @@ GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
 # (tests/golden/reference_runs.json, the reference built from its sources) or,
 # for Chebyshev(8) which the reference does not have, the restatement's
 GOLDEN_OF = {
-    (4096, 95, "identity", "mgsr"): ("reference_runs.json", "mgsr_omp_identity_4096_m95_1cyc_t8"),
-    (1024, 95, "identity", "mgsr"): ("reference_runs.json", "mgsr_omp_identity_1024_m95_3cyc_t8"),
+    (4096, 95, "identity", "mgsr"): ("reference_runs.json", "mgsr_omp_identity_4096_m95_2cyc_t8"),
+    (1024, 95, "identity", "mgsr"): ("reference_runs.json", "mgsr_omp_identity_1024_m95_12cyc_t8"),
     (4096, 95, "cheb", "mgsr"): ("oracle_4096.json", "mgsr_cheb8"),
-    (4096, 95, "cbpr2", "mgsr"): ("reference_runs.json", "mgsr_omp_cbpr2_4096_m95_1cyc_t8"),
-    (4096, 95, "identity", "hh"): ("reference_runs.json", "hh_omp_identity_4096_m95_1cyc_t8"),
+    (4096, 95, "cbpr2", "mgsr"): ("reference_runs.json", "mgsr_omp_cbpr2_4096_m95_2cyc_t8"),
+    (4096, 95, "identity", "hh"): ("reference_runs.json", "hh_omp_identity_4096_m95_2cyc_t8"),
+}
+# older fixtures (cycle 1 only / 3 cycles) where a longer history is not recorded
+GOLDEN_FALLBACK = {
+    "mgsr_omp_identity_4096_m95_2cyc_t8": "mgsr_omp_identity_4096_m95_1cyc_t8",
+    "mgsr_omp_identity_1024_m95_12cyc_t8": "mgsr_omp_identity_1024_m95_3cyc_t8",
+    "mgsr_omp_cbpr2_4096_m95_2cyc_t8": "mgsr_omp_cbpr2_4096_m95_1cyc_t8",
+    "hh_omp_identity_4096_m95_2cyc_t8": "hh_omp_identity_4096_m95_1cyc_t8",
 }
 # (BASELINE configs[] index, grid, precond, degree, method, timed cycles)
 CONFIG_LEGS = [(1, 1024, "identity", 1, "mgsr", 3), (2, 4096, "cheb", 8, "mgsr", 2), (4, 4096, "identity", 1, "hh", 2)]
 
 
-def cycle1_vs_golden(r1: float, gfile: str | None, gkey: str | None, tol: float = 1e-9) -> dict:
-    if gfile is None:
-        return {"cycle1_true_rel_residual": r1}
-    g = json.load(open(os.path.join(GOLDEN_DIR, gfile)))[gkey]["hist_res"][0]
-    dev = abs(r1 - g) / g
-    return {"cycle1_true_rel_residual": r1, "golden": g, "golden_source": f"tests/golden/{gfile}:{gkey}",
-            "rel_dev": dev, "tol": tol, "pass": bool(dev <= tol)}
+def history_vs_golden(hist, gfile: str | None, gkey: str | None, tol: float = 1e-9, floor: float = 1e-6) -> dict:
+    """The per-cycle true relative residuals of a run from x0 = 0 against the
+    golden run's (the reference's own, or for Chebyshev(8) the restatement's):
+    every common cycle within `tol` relative while the residual is above
+    `floor` (below it the history is chaotic)."""
+    hist = [float(h) for h in hist]
+    if gfile is None or not hist:
+        return {"cycle1_true_rel_residual": hist[0] if hist else None}
+    runs = json.load(open(os.path.join(GOLDEN_DIR, gfile)))
+    if gkey not in runs:
+        gkey = GOLDEN_FALLBACK.get(gkey, gkey)
+    g = runs[gkey]["hist_res"]
+    k = min(len(hist), len(g))
+    devs = [abs(hist[i] - g[i]) / g[i] for i in range(k)]
+    checked = [d for i, d in enumerate(devs) if g[i] > floor]
+    return {"cycle1_true_rel_residual": hist[0], "golden": g[0], "golden_source": f"tests/golden/{gfile}:{gkey}",
+            "rel_dev": devs[0], "cycles_compared": k, "history": hist[:k], "history_rel_dev": devs,
+            "tol": tol, "pass": bool(checked and max(checked) <= tol)}
 
 
 def config_legs(ga, prof_every: int) -> list[dict]:
@@ -517,7 +603,7 @@ def config_legs(ga, prof_every: int) -> list[dict]:
                 return ga.gmres_hh(c, 1e-15, precondition=prec != "identity", max_cycles=k, want_verr=False,
                                    want_hist=hist, want_x=want_x)
 
-            chk = run(1, hist=True)
+            chk = run(K, hist=True)  # from x0 = 0: the K cycles' residual history vs the golden run
             c.profile(1 if method == "hh" else max(1, prof_every))
             c.profile_reset()
             c.sync()
@@ -526,16 +612,17 @@ def config_legs(ga, prof_every: int) -> list[dict]:
             c.sync()
             t1 = time.perf_counter()
             prof = c.profile_read()
-            sten = method == "mgsr" and c.res_info().get("sten", 0) == 1
-            roof = roofline_entry(prof, ns, c.nloc, r.n_cycles, 1, sten) or {}
+            plan = c.res_info(hh=method == "hh")
+            sten = method == "mgsr" and plan.get("sten", 0) == 1
+            roof = roofline_entry(prof, ns, c.nloc, r.n_cycles, 1, plan, sten) or {}
         iters = (r.n_cycles - 1) * m + r.n_out
         pname = {"identity": "no precond", "cbpr2": "cbpr2", "cheb": f"Chebyshev({degree})"}[prec]
         leg = {"baseline_config": idx, "workload": f"{N}x{N} Poisson-2D fp64, GMRES-{method.upper()} m={m}, {pname}",
                "it_s": round(iters / (t1 - t0), 3), "ms_per_cycle": round((t1 - t0) / r.n_cycles * 1e3, 3),
                "cycles": r.n_cycles,
-               "dominant": {k: roof.get(k) for k in ("kernel", "avg_launch_us", "per_projection_us", "achieved",
-                                                     "frac")},
-               "check": cycle1_vs_golden(chk.hist_res[0], *GOLDEN_OF[(N, m, prec, method)])}
+               "dominant": {k: roof.get(k) for k in ("kernel", "variant", "avg_launch_us", "per_projection_us",
+                                                     "achieved", "bound", "peak", "frac", "hbm_spec_frac")},
+               "check": history_vs_golden(chk.hist_res, *GOLDEN_OF[(N, m, prec, method)])}
         if prof.get("prec", (0, 0))[1] > 0:  # the temporal-blocked Chebyshev pass (k_cheb_fused)
             us = prof["prec"][0] * 1e3 / prof["prec"][1]
             leg["chebyshev_pass"] = {"avg_launch_us": round(us, 2), "launches_sampled": prof["prec"][1],
@@ -558,9 +645,10 @@ def main() -> None:
     ap.add_argument("--method", default="mgsr", choices=["mgsr", "hh"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-cap", type=float, default=45.0,
-                    help="seconds: all-core reference leg runs a full cycle if it finishes within this, else a sample")
-    ap.add_argument("--cpu-cap-leg", type=float, default=8.0,
-                    help="seconds of cycle 1 sampled per thread-sweep leg below the process's OpenMP share")
+                    help="seconds: the share's leg also runs one full cycle (a check of the fit) if the fit says it "
+                         "finishes within this")
+    ap.add_argument("--cpu-steps", type=int, default=24,
+                    help="Arnoldi steps of cycle 1 every thread-sweep leg times (the same window for every leg)")
     ap.add_argument("--no-configs", action="store_true",
                     help="N=1: skip the short timed legs of BASELINE configs 2, 3 and 5 after the headline")
     ap.add_argument("--no-prof", action="store_true", help="no HIP-event kernel timing in the timed region")
@@ -576,8 +664,8 @@ def main() -> None:
     args = ap.parse_args()
     maybe_self_launch(args, sys.argv[1:])
 
-    import torch  # device plumbing + gloo control plane only
-
+    # No torch in this process: the library runs on the HIP runtime and RCCL it
+    # was built against (gmres_amd._native; the line's config.runtime says which).
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -589,11 +677,9 @@ def main() -> None:
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
+    from gmres_amd.ctl import Ctl
 
-        dist.init_process_group("gloo")
+    ctl = Ctl(rank, world)  # out-of-band control plane (TCP on loopback); a no-op for one rank
 
     import gmres_amd as ga
 
@@ -609,19 +695,14 @@ def main() -> None:
     if world > 1 and args.collective == "xgmi":
         ctx.comm_init_xgmi(world, rank, ml)
     elif world > 1 or os.environ.get("GK_FORCE_RCCL") == "1":  # 1-rank RCCL: exercises the comm path
-        obj = [ga.Context.unique_id() if rank == 0 else None]
-        if dist is not None:
-            dist.broadcast_object_list(obj, src=0)
+        uid = ctl.bcast(ga.Context.unique_id() if rank == 0 else None)
         ok, why = 1, ""
         try:
-            ctx.comm_init(world, rank, ml, obj[0])
+            ctx.comm_init(world, rank, ml, uid)
         except ga.GkError as e:
             ok, why = 0, str(e)
             print(f"rank {rank}: RCCL communicator failed: {e}", file=sys.stderr)
-        if dist is not None:
-            t = torch.tensor([ok], dtype=torch.int32)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            ok = int(t.item())
+        ok = ctl.allreduce(ok, "min")
         if ok:
             collective = "rccl"
         elif world > 1 and args.collective == "auto":
@@ -632,7 +713,7 @@ def main() -> None:
         else:
             raise RuntimeError(f"RCCL communicator: {why or 'a peer rank failed'}")
     if world > 1 and args.collective in ("auto", "xgmi"):
-        collective = setup_xgmi(ctx, dist, world, rank,
+        collective = setup_xgmi(ctx, ctl, rank,
                                 required=args.collective == "xgmi" or rccl_failed is not None) or "rccl"
     for kv in args.tune:
         k, v = kv.split("=")
@@ -647,10 +728,8 @@ def main() -> None:
                            want_verr=False, want_hist=hist, want_x=want_x)
 
     def barrier():
-        ctx.sync()
-        torch.cuda.synchronize(local)
-        if dist is not None:
-            dist.barrier()
+        ctx.sync()  # this rank's stream drained (every kernel of the solve is on it)
+        ctl.barrier()
 
     warm = {}
 
@@ -663,19 +742,21 @@ def main() -> None:
             why = str(e)
             print(f"rank {rank}: warmup failed: {e}", file=sys.stderr)
             ok = 0
-        if dist is not None:
-            t = torch.tensor([ok], dtype=torch.int32)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            ok = int(t.item())
-        return ok == 1, why
+        return ctl.allreduce(ok, "min") == 1, why
 
     fallback = None
     ok, why = guarded_warmup()
     if not ok:
         # Fallback, decided by all ranks together and REPORTED in the JSON line:
-        # the launch-per-projection path (and RCCL instead of the device exchange).
+        # the launch-per-projection path, and RCCL instead of the device exchange
+        # where an RCCL communicator exists.  A device exchange that missed a
+        # deadline is retired (its sequence numbers may differ across ranks), so
+        # without RCCL there is nothing to fall back to: fail with both reasons.
         fallback = {"reason": why[:300] or "a peer rank failed its warmup", "to": "launch-per-projection path"}
-        if collective == "xgmi-device-exchange" and args.collective == "auto":
+        if collective == "xgmi-device-exchange":
+            if rccl_failed is not None or args.collective == "xgmi":
+                raise RuntimeError(f"warmup failed on the device exchange ({fallback['reason']}) and there is no "
+                                   f"RCCL communicator to fall back to ({rccl_failed or '--collective xgmi'})")
             ctx.xchg_enable(False)
             collective = "rccl"
             fallback["to"] += " + RCCL (device exchange failed in warmup)"
@@ -694,19 +775,18 @@ def main() -> None:
     prof = ctx.profile_read() if not args.no_prof else {}
     resid = ctx.true_residual()  # outside the timed region; same value at any N
     comm = ctx.comm_info()
-    elapsed = t1 - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = ctl.allreduce(t1 - t0, "max")
     cycles = res.n_cycles
     iters = (cycles - 1) * m + res.n_out if cycles > 0 else 0
-    diag = None if args.no_diag else diagnostics(ctx, args, run, dist, world)
+    plan = ctx.res_info(hh=args.method == "hh")  # the resident variant the timed launches ran
+    diag = None if args.no_diag else diagnostics(ctx, args, run, ctl, world)
     if diag is not None:
-        diag["pcie_inclusive"] = pcie_inclusive(ctx, args, run, dist, line0, nlines)
+        diag["pcie_inclusive"] = pcie_inclusive(ctx, args, run, ctl, line0, nlines)
 
-    sten = args.method == "mgsr" and ctx.res_info().get("sten", 0) == 1
-    roof = roofline_entry(prof, args, ctx.nloc, cycles, world, sten) if rank == 0 else None
+    sten = args.method == "mgsr" and plan.get("sten", 0) == 1
+    cheb_sten = plan.get("cheb_sten", 0) == 1
+    roof = roofline_entry(prof, args, ctx.nloc, cycles, world, plan, sten) if rank == 0 else None
+    runtime = ga.runtime_info()
     ctx.close()
     legs = None
     if rank == 0 and world == 1 and not args.no_configs and (N, m, args.prec, args.method) == (4096, 95, "identity",
@@ -716,15 +796,15 @@ def main() -> None:
         n = N * N
         it_s = iters / elapsed
         full = cycles == args.steps and res.n_out == m
-        b_fused = cycle_bytes(n, m, args.prec, args.degree, args.method, "fused", sten) * cycles
+        b_fused = cycle_bytes(n, m, args.prec, args.degree, args.method, "fused", sten, cheb_sten) * cycles
         b_written = cycle_bytes(n, m, args.prec, args.degree, args.method, "as_written", sten) * cycles
         cpu = None
         if not args.no_cpu and world == 1:
-            cpu = cpu_baseline(N, m, args.prec, args.degree, args.method, args.cpu_cap, args.cpu_cap_leg)
+            cpu = cpu_baseline(N, m, args.prec, args.degree, args.method, args.cpu_cap, args.cpu_steps)
         check = {"true_rel_residual_after_timed_cycles": resid}
         if "res" in warm and len(warm["res"].hist_res) > 0:
-            check.update(cycle1_vs_golden(warm["res"].hist_res[0], *GOLDEN_OF.get((N, m, args.prec, args.method),
-                                                                                 (None, None))))
+            check.update(history_vs_golden(warm["res"].hist_res, *GOLDEN_OF.get((N, m, args.prec, args.method),
+                                                                                (None, None))))
         prec_name = {"identity": "no precond", "cbpr2": "cbpr2", "cheb": f"Chebyshev({args.degree})"}[args.prec]
         out = {
             "metric": METRIC,
@@ -744,7 +824,9 @@ def main() -> None:
                        "step": "one GMRES(m) restart cycle", "parallelism": f"row-block slabs x{world}",
                        "collective": collective, "comm_ranks_seen": comm["nranks"], "comm_kind": comm["kind"],
                        "rccl_init_failed": rccl_failed,
-                       "arnoldi_iters": iters},
+                       "resident_variant": plan.get("variant"), "resident_workgroups": plan.get("G"),
+                       "arnoldi_iters": iters,
+                       "runtime": runtime},
             "fallback": fallback,
             "check": check,
             "hbm_gbps_fused": round(b_fused / elapsed / 1e9, 1) if full else None,
@@ -757,9 +839,8 @@ def main() -> None:
             "configs": legs,
         }
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    ctl.barrier()
+    ctl.close()
 
 
 if __name__ == "__main__":

@@ -32,12 +32,13 @@ GK_TUNE_CHEB_STEN = 16
 GK_TUNE_RES_STEN = 17
 GK_TUNE_SPIN_WAIT = 18
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
-GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES, GK_KID_PREC = range(8)
-KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res", "prec"]
+(GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES, GK_KID_PREC,
+ GK_KID_HALO) = range(9)
+KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res", "prec", "halo"]
 COMM_KINDS = {0: None, 1: "rccl", 2: "local-group", 3: "xgmi-device-exchange"}
 # resident-step variants (gk_res_info / gk_res_plan_query)
 RES_VARIANTS = {0: None, 1: "prefetch", 2: "pairs", 3: "pairs+lds", 4: "w-only"}
-RES_INFO_KEYS = ["variant", "G", "r2", "l2", "pf", "cw", "wo", "nt", "r2e", "l2e", "lds", "nres2", "sten"]
+RES_INFO_KEYS = ["variant", "G", "r2", "l2", "pf", "cw", "wo", "nt", "r2e", "l2e", "lds", "nres2", "sten", "cheb_sten"]
 
 c_int, c_double, c_ll, c_vp = ctypes.c_int, ctypes.c_double, ctypes.c_longlong, ctypes.c_void_p
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -60,6 +61,7 @@ def header_symbols() -> list[str]:
 _SIGS = {
     "gk_last_error": (ctypes.c_char_p, []),
     "gk_version": (c_int, []),
+    "gk_runtime_info": (c_int, [_ip, _ip, _ip, ctypes.c_char_p, ctypes.c_char_p, c_int]),
     "gk_create": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_vp)]),
     "gk_destroy": (c_int, [c_vp]),
     "gk_comm_unique_id": (c_int, [ctypes.c_char_p]),
@@ -129,20 +131,55 @@ _FSIGS = {
 }
 
 
+class _TorchAfterNative:
+    """Import guard, installed once this library runs on /opt/rocm's HIP runtime
+    in a process that had not imported torch: torch bundles its own
+    libamdhip64 / libhsa-runtime64 / librccl and loads them by path, so
+    importing it now would put a second HIP runtime into the process (measured:
+    the process aborts at exit, "double free or corruption").  Fail at the
+    import instead, with the remedy."""
+
+    def find_spec(self, name, path=None, target=None):
+        if name == "torch":
+            raise ImportError("gmres_amd already runs on " + (runtime_paths().get("hip") or "/opt/rocm's HIP runtime")
+                              + "; importing torch now would load torch's bundled HIP runtime as a second one. "
+                                "Import torch before gmres_amd's first native call (then torch's runtime is "
+                                "used), or keep this process torch-free.")
+        return None
+
+
+def runtime_paths() -> dict:
+    """The HIP / RCCL / HSA libraries this process has mapped (/proc/self/maps)."""
+    out = {}
+    try:
+        for line in open("/proc/self/maps"):
+            f = line.split()[-1] if len(line.split()) >= 6 else ""
+            for key, stem in (("hip", "libamdhip64.so"), ("rccl", "librccl.so"), ("hsa", "libhsa-runtime64.so")):
+                if stem in os.path.basename(f):
+                    out.setdefault(key, f)
+    except OSError:
+        pass
+    return out
+
+
 def _one_hip_runtime() -> None:
-    """torch bundles its own libamdhip64 / libhsa-runtime64 / librccl and loads
-    them by path.  Loaded after this library (which links /opt/rocm's), they
-    would be a second HIP runtime in the process -- measured: the process
-    aborts at exit (double free).  Loaded first, their sonames satisfy this
-    library's and the process has one runtime.  So torch, when installed, is
-    imported before the first native load (it is device plumbing for the
-    harness and the tests; the product itself does not use it)."""
+    """One HIP runtime per process.  The product runs on the runtime it was
+    built against (/opt/rocm, the NEEDED entries of libgmres_hip.so) and never
+    imports torch.  If the caller imported torch first, torch's bundled
+    runtime is already mapped and satisfies this library's sonames (one
+    runtime: torch's; gk_runtime_info / runtime_paths() say which).  If not,
+    a later `import torch` is refused (_TorchAfterNative).  GK_TORCH_FIRST=1
+    restores the rounds-1..3 behaviour: import torch here, before the load."""
     if "torch" in sys.modules:
         return
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    if os.environ.get("GK_TORCH_FIRST") == "1":
+        try:
+            import torch  # noqa: F401
+            return
+        except ImportError:
+            pass
+    if not any(isinstance(f, _TorchAfterNative) for f in sys.meta_path):
+        sys.meta_path.insert(0, _TorchAfterNative())
 
 
 def _load(path: str, what: str) -> ctypes.CDLL:
@@ -176,6 +213,18 @@ def fhost() -> ctypes.CDLL:
             f.argtypes = args
         _fhost = L
     return _fhost
+
+
+def runtime_info() -> dict:
+    """The runtime the product is running on: HIP runtime / driver and RCCL
+    versions (gk_runtime_info) and the library files mapped for them."""
+    a, b, c = c_int(), c_int(), c_int()
+    hp, rp = ctypes.create_string_buffer(512), ctypes.create_string_buffer(512)
+    check(hip().gk_runtime_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), hp, rp, 512), "gk_runtime_info")
+    maps = runtime_paths()
+    return {"hip_runtime_version": a.value, "hip_driver_version": b.value, "rccl_version": c.value,
+            "libamdhip64": hp.value.decode() or maps.get("hip"), "librccl": rp.value.decode() or maps.get("rccl"),
+            "libhsa_runtime64": maps.get("hsa"), "torch_imported": "torch" in sys.modules}
 
 
 def last_error() -> str:

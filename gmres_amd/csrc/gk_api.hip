@@ -7,6 +7,7 @@
 // Hessenberg entries of each Arnoldi step.  All work is issued on one HIP
 // stream per context; on N GPUs the dot-product slabs are RCCL all-reduced
 // and the stencil halos exchanged point-to-point on that same stream.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -427,7 +428,7 @@ int halo_lines(gk_ctx *c, const double *vec, int nl, double *lo, double *hi) {
     // neighbours would need lines from two ranks away)
     if (c->nranks > 1 && (nl < 1 || nl > c->nlines))
         return set_err(GK_ERR_ARG, "halo of %d lines from a slab of %d lines (rank %d)", nl, c->nlines, c->rank);
-    ProfScope ps(c, GK_KID_COMM);
+    ProfScope ps(c, GK_KID_HALO);
     const int N = c->N;
     const i64 cnt = (i64)nl * N;
     if (c->xs_on) {
@@ -735,7 +736,8 @@ bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
 }
 
 // gk_res_plan_query / gk_res_info layout
-enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, RPI_R2E, RPI_L2E, RPI_LDS, RPI_NRES2, RPI_STEN };
+enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, RPI_R2E, RPI_L2E, RPI_LDS, RPI_NRES2, RPI_STEN,
+       RPI_CHEB_STEN };
 void plan_info(const ResPlan &p, bool on, long long *info) {
     for (int k = 0; k < GK_RES_INFO_LEN; ++k) info[k] = 0;
     if (!on) return;
@@ -1279,6 +1281,23 @@ extern "C" {
 const char *gk_last_error(void) { return g_err.c_str(); }
 int gk_version(void) { return 1; }
 
+int gk_runtime_info(int *hip_runtime, int *hip_driver, int *rccl, char *hip_path, char *rccl_path, int len) {
+    if (hip_runtime == nullptr || hip_driver == nullptr || rccl == nullptr) return set_err(GK_ERR_ARG, "null argument");
+    *hip_runtime = *hip_driver = *rccl = 0;
+    HIPCHK(hipRuntimeGetVersion(hip_runtime));
+    HIPCHK(hipDriverGetVersion(hip_driver));
+    NCCLCHK(ncclGetVersion(rccl));
+    auto path_of = [&](const void *sym, char *out) {
+        if (out == nullptr || len <= 0) return;
+        Dl_info di{};
+        const char *p = (dladdr(sym, &di) != 0 && di.dli_fname != nullptr) ? di.dli_fname : "";
+        std::snprintf(out, (size_t)len, "%s", p);
+    };
+    path_of(reinterpret_cast<const void *>(&hipRuntimeGetVersion), hip_path);
+    path_of(reinterpret_cast<const void *>(&ncclGetVersion), rccl_path);
+    return GK_OK;
+}
+
 int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out) {
     if (out == nullptr) return set_err(GK_ERR_ARG, "null out");
     *out = nullptr;
@@ -1464,7 +1483,9 @@ int gk_comm_init_xgmi(gk_ctx *c, int nranks, int rank, int max_lines) {
         return set_err(GK_ERR_ARG, "bad xgmi comm args (nranks <= %d)", gk::XS_MAXR);
     HIPCHK(hipSetDevice(c->dev));
     if (c->comm != nullptr) {  // an RCCL communicator of an abandoned gk_comm_init: the exchange replaces it
-        ncclCommDestroy(c->comm);
+        // abort, not destroy: ncclCommDestroy finalises collectively and can wait on
+        // peers whose init failed or that have moved on; ncclCommAbort is local
+        ncclCommAbort(c->comm);
         c->comm = nullptr;
         c->comm_ok = false;
     }
@@ -1510,16 +1531,38 @@ int gk_xchg_open(gk_ctx *c, const unsigned char *handles) {
     return GK_OK;
 }
 
+// Hardware queues HIP gives this process per device: GPU_MAX_HW_QUEUES, else
+// HIP's default of 4.
+int hw_queues() {
+    const char *e = std::getenv("GPU_MAX_HW_QUEUES");
+    const int q = (e != nullptr && *e != '\0') ? std::atoi(e) : 4;
+    return q > 0 ? q : 4;
+}
+
 int gk_xchg_local(gk_ctx *c) {
     if (c == nullptr || c->lg == nullptr) return set_err(GK_ERR_STATE, "gk_xchg_local needs gk_comm_init_local");
     if (c->nranks > gk::XS_MAXR) return set_err(GK_ERR_ARG, "device exchange supports <= %d ranks", gk::XS_MAXR);
     std::lock_guard<std::mutex> lk(c->lg->mu);
+    int same_dev = 0;
     for (int r = 0; r < c->nranks; ++r) {
         gk_ctx *o = c->lg->members[r];
         if (o == nullptr || o->xs_buf == nullptr)
             return set_err(GK_ERR_STATE, "rank %d of the group has not joined yet", r);
-        c->xs_peers.p[r] = o->xs_buf;
+        same_dev += o->dev == c->dev;
     }
+    // Every in-process rank on this device spins on its peers' granules from its
+    // own stream: the streams must not share a hardware queue, or a spinning
+    // exchange kernel can sit in front of its peer's kernel until the deadline
+    // (seen with 4 ranks under HIP's default of 4 queues).  One more stream (the
+    // null stream) may hold a queue too.
+    const int q = hw_queues();
+    if (same_dev + 1 > q)
+        return set_err(GK_ERR_STATE,
+                       "%d in-process ranks on device %d (+1 stream) need more than the %d hardware queues of this "
+                       "process (GPU_MAX_HW_QUEUES): their spinning exchange kernels would deadlock; set "
+                       "GPU_MAX_HW_QUEUES >= %d before the HIP runtime starts",
+                       same_dev, c->dev, q, same_dev + 1);
+    for (int r = 0; r < c->nranks; ++r) c->xs_peers.p[r] = c->lg->members[r]->xs_buf;
     c->xs_ready = true;
     c->xs_on = true;
     return GK_OK;
@@ -2360,6 +2403,13 @@ int gk_res_info(gk_ctx *c, int hh, long long *info) {
     const bool on = res_plan(c, p, hh != 0);
     plan_info(p, on, info);
     info[RPI_STEN] = on && hh == 0 && res_sten(c, p) ? 1 : 0;
+    // op_precond_sten's conditions, without its collective (the smallest slab of
+    // a multi-rank context is gathered at its first solve)
+    int cs = c->pkind == GK_PREC_CHEB && c->tune_cheb_sten && c->pdeg <= gk::CF_LMAX && c->N >= gk::CF_PTS &&
+             c->tune_cheb_fused && c->N % 2 == 0 &&
+             (i64)c->N * std::max(c->nlines, c->max_lines) * 8 < (1LL << 31);
+    if (cs && collective(c) && c->nranks > 1) cs = c->min_lines == 0 ? -1 : (c->min_lines >= c->pdeg + 1 ? 1 : 0);
+    info[RPI_CHEB_STEN] = cs;
     return GK_OK;
 }
 

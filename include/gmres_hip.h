@@ -50,17 +50,23 @@ extern "C" {
 #define GK_KID_STENCIL 1 /* Poisson-5 stencil sweeps incl. fused preconditioner sweeps */
 #define GK_KID_SCALE 2   /* normalisation V(:,j+1) = w / h */
 #define GK_KID_UPDATE 3  /* x += V y */
-#define GK_KID_COMM 4    /* all-reduce / halo / broadcast (RCCL or device exchange) */
+#define GK_KID_COMM 4    /* all-reduce / broadcast (RCCL, local group or device exchange) */
 #define GK_KID_OTHER 5
 #define GK_KID_RES 6     /* resident MGS-R step: whole cascade + norm + scale in one launch */
 #define GK_KID_PREC 7    /* temporal-blocked Chebyshev(k) passes (k_cheb_fused) */
-#define GK_NKID 8
+#define GK_KID_HALO 8    /* halo lines with the slab neighbours (RCCL send/recv, local group or device exchange) */
+#define GK_NKID 9
 
 typedef struct gk_ctx gk_ctx;
 typedef struct gk_group gk_group;
 
 const char *gk_last_error(void);
 int gk_version(void);
+/* Which runtime this library is running on (bench.py / smoke() report it):
+ * hipRuntimeGetVersion, hipDriverGetVersion, ncclGetVersion, and the files the
+ * process mapped for libamdhip64 and librccl (dladdr of one of their symbols),
+ * NUL-terminated into hip_path / rccl_path (capacity `len` bytes each). */
+int gk_runtime_info(int *hip_runtime, int *hip_driver, int *rccl, char *hip_path, char *rccl_path, int len);
 
 /* ------------------------------------------------------------ context ---- */
 /* Create a context on HIP device `device` for an N x N grid, owning lines
@@ -91,7 +97,13 @@ int gk_comm_init_local(gk_ctx *ctx, gk_group *g, int rank, int max_lines);
  *   gk_xchg_open        map every rank's region (handles: nranks x 64 bytes,
  *                       rank order) and route collectives through it;
  *   gk_xchg_local       the same for a gk_group (in-process, after every
- *                       member's gk_comm_init_local);
+ *                       member's gk_comm_init_local); GK_ERR_STATE at once
+ *                       when the members on this device, plus one stream
+ *                       (the null stream), exceed the process's hardware
+ *                       queues (GPU_MAX_HW_QUEUES, HIP's default 4): streams
+ *                       would share a queue, and a spinning exchange kernel
+ *                       could sit in front of its peer's kernel until the
+ *                       deadline;
  *   gk_xchg_enable      0: back to RCCL / the local group, 1: device exchange;
  *   gk_xchg_selftest    collective check of the reduction and halo paths with
  *                       a deadline; GK_ERR_COMM if any granule is missing or
@@ -266,7 +278,10 @@ int gk_sync(gk_ctx *ctx);
  * info[GK_RES_INFO_LEN]: variant, workgroups G, R2, L2, prefetch, control
  * wave, w-only, non-temporal column loads, register / LDS chunks per
  * workgroup in use, dynamic LDS bytes, resident double2 of the slab, and
- * (gk_res_info only) whether the MGS step launch forms w = A V(:,j) itself.
+ * (gk_res_info only) whether the MGS step launch forms w = A V(:,j) itself,
+ * and whether the Arnoldi step's Chebyshev(k) pass forms z = A v in its own
+ * stage 0 (1 / 0; -1 on a multi-rank context whose smallest slab is not known
+ * until its first solve).
  * gk_res_plan_query: pure host computation for a slab of nloc unknowns on a
  * device with `cus` compute units shared by `share` contexts; hh != 0 the
  * reflection chains' plan; nt: -1 auto (from nloc), 0 / 1 forced.  No device
@@ -278,7 +293,7 @@ int gk_sync(gk_ctx *ctx);
 #define GK_RES_PAIRS 2
 #define GK_RES_PAIRS_LDS 3
 #define GK_RES_WONLY 4
-#define GK_RES_INFO_LEN 13
+#define GK_RES_INFO_LEN 14
 int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, long long *info);
 int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 

@@ -11,10 +11,15 @@ contexts joined by one of the two multi-rank transports:
          concurrently: test_gpu_configs.py starts this module as a child
          process with GPU_MAX_HW_QUEUES=16 (HIP's default of 4 hardware
          queues would serialise streams that share a queue).
+  xchg-res  the device exchange with the resident step forced on
+         (GK_TUNE_RES 1, GK_TUNE_RES_SHARE 8: 32 workgroups per rank): every
+         Arnoldi step is ONE launch per rank whose 2j projections sum the 8
+         rank totals inside the launch -- the in-launch cross-rank path the
+         8-GPU run takes (there with 256 workgroups per rank).
 
 Prints one JSON line: the single run's and rank 0's residual / final_err,
 whether every rank took identical decisions, and the largest deviations.
-  python tests/config4_run.py local|xchg
+  python tests/config4_run.py local|xchg|xchg-res
 """
 from __future__ import annotations
 
@@ -48,12 +53,18 @@ def run(transport: str) -> dict:
         ml = max(nl for _, nl in parts)
         for r, c in enumerate(ctxs):
             c.comm_init_local(g, r, ml)
-        if transport == "xchg":
+        if transport in ("xchg", "xchg-res"):
             for c in ctxs:
                 c.xchg_local()
                 c.tune(nat.GK_TUNE_XCHG_TIMEOUT_MS, 20000)
+        if transport == "xchg-res":
+            for c in ctxs:
+                c.tune(nat.GK_TUNE_RES, 1)
+                c.tune(nat.GK_TUNE_RES_SHARE, R)
+                c.tune(nat.GK_TUNE_RES_TIMEOUT_MS, 20000)
         kinds = {c.comm_info()["kind"] for c in ctxs}
         plans = {c.res_info()["variant"] for c in ctxs}
+        gs = {c.res_info()["G"] for c in ctxs}
 
         def work(r):
             try:
@@ -76,7 +87,11 @@ def run(transport: str) -> dict:
         x = np.concatenate([o.x for o in res])
         return {
             "ok": True, "transport": transport, "comm_kinds": sorted(map(str, kinds)), "res_variants": sorted(map(str, plans)),
+            "res_G": sorted(gs),
             "comm_launches": int(min(o[1]["comm"][1] for o in out)),
+            "comm_launches_max": int(max(o[1]["comm"][1] for o in out)),
+            "res_launches_min": int(min(o[1]["res"][1] for o in out)),
+            "proj_launches_max": int(max(o[1]["proj"][1] for o in out)),
             "same_decisions": len({(o.n_out, o.cycles_out, o.n_cycles) for o in res}) == 1
             and all(np.array_equal(o.hist_res, res[0].hist_res) for o in res)
             and all(np.array_equal(o.final_err, res[0].final_err) for o in res),

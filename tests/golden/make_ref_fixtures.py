@@ -5,6 +5,8 @@ modules compiled from /root/reference/src, see oracle/Makefile.ref).
 Build container only (needs the compiled reference).  The fixtures are data:
 per-cycle true residuals, final_err(1:n_out), v_err, iteration counts, x (full
 at N <= 64).  Run:  python tests/golden/make_ref_fixtures.py [--quick]
+                    python tests/golden/make_ref_fixtures.py --only KEY[,KEY...]
+(--only re-runs the named cases and merges them into the existing files.)
 """
 from __future__ import annotations
 
@@ -56,6 +58,14 @@ THREADED = [
     ("mgsr_omp_identity_4096_m95_1cyc_t8", "mgsr_omp", 4096, 95, "identity", 8, 1),
     ("mgsr_omp_cbpr2_4096_m95_1cyc_t8", "mgsr_omp", 4096, 95, "cbpr2", 8, 1),
     ("hh_omp_identity_4096_m95_1cyc_t8", "hh_omp", 4096, 95, "identity", 8, 1),
+    # residual HISTORIES beyond cycle 1 (round 4): the two cycles the bench legs time at
+    # 4096^2, and twelve cycles at config-2 size
+    ("mgsr_omp_identity_4096_m95_2cyc_t8", "mgsr_omp", 4096, 95, "identity", 8, 2),
+    ("mgsr_omp_cbpr2_4096_m95_2cyc_t8", "mgsr_omp", 4096, 95, "cbpr2", 8, 2),
+    ("hh_omp_identity_4096_m95_2cyc_t8", "hh_omp", 4096, 95, "identity", 8, 2),
+    ("mgsr_omp_identity_1024_m95_12cyc_t8", "mgsr_omp", 1024, 95, "identity", 8, 12),
+    ("mgsr_omp_cbpr2_1024_m95_12cyc_t8", "mgsr_omp", 1024, 95, "cbpr2", 8, 12),
+    ("hh_omp_identity_1024_m95_12cyc_t8", "hh_omp", 1024, 95, "identity", 8, 12),
 ]
 
 
@@ -76,8 +86,14 @@ def record(key, solver, N, m, prec, threads, max_cycles):
 
 def main() -> None:
     quick = "--quick" in sys.argv
+    only = None
+    if "--only" in sys.argv:
+        only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
+        unknown = only - {c[0] for c in SMALL + THREADED}
+        if unknown:
+            raise SystemExit(f"unknown cases {sorted(unknown)}")
     refrun.build()
-    small = [c for c in SMALL if not quick or c[2] <= 128]
+    small = [c for c in SMALL if (not quick or c[2] <= 128) and (only is None or c[0] in only)]
     out, xs = {}, {}
     with ThreadPoolExecutor(6) as ex:
         for key, d, x in ex.map(lambda c: record(*c), small):
@@ -85,7 +101,7 @@ def main() -> None:
             if x is not None:
                 xs[key] = x
     for c in THREADED:
-        if quick and c[2] > 128:
+        if (quick and c[2] > 128) or (only is not None and c[0] not in only):
             continue
         key, d, x = record(*c)
         out[key] = d
@@ -97,11 +113,16 @@ def main() -> None:
                        "oracle/ref_driver.f90; b = A*1, x0 = 0, tol 1e-15 (CG/BiCGSTAB 1e-9), params (8.2, 0.2)",
             "_generator": "tests/golden/make_ref_fixtures.py"}
     path = os.path.join(HERE, "reference_runs.json")
-    old = json.load(open(path)) if os.path.exists(path) and quick else {}
+    merge = quick or only is not None
+    old = json.load(open(path)) if os.path.exists(path) and merge else {}
     old.update(out)
     old.update(meta)
     json.dump(dict(sorted(old.items())), open(path, "w"), indent=1)
-    np.savez_compressed(os.path.join(HERE, "reference_x.npz"), **xs)
+    xpath = os.path.join(HERE, "reference_x.npz")
+    if merge and os.path.exists(xpath):
+        with np.load(xpath) as f:
+            xs = {**{k: f[k] for k in f.files}, **xs}
+    np.savez_compressed(xpath, **xs)
 
 
 if __name__ == "__main__":

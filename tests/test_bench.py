@@ -64,6 +64,43 @@ def test_byte_models():
     # Chebyshev(16) hands (d, r, z) from the first pass to the second
     assert bench.prec_bytes(n, "cheb", 8, "fused") == 0 and bench.prec_bytes(n, "cheb", 8, "as_written") == 384 * n
     assert bench.prec_bytes(n, "cheb", 16, "fused") == 64 * n
+    # without the stencil stage (GK_TUNE_CHEB_STEN 0, N < 128, thin slabs) the pass
+    # reads z from a stencil launch: +16n
+    assert bench.prec_bytes(n, "cheb", 8, "fused", cheb_sten=False) == 16 * n
+    assert (bench.cycle_bytes(n, 95, "cheb", 8, "mgsr", "fused", cheb_sten=False)
+            - bench.cycle_bytes(n, 95, "cheb", 8, "mgsr", "fused")) == 95 * 16 * n
+
+
+def _plan(N, R=1, share=1, nt=-1):
+    import gmres_amd as ga
+
+    nl = max(k for _, k in ga.slab_partition(N, R))
+    return N * nl, ga.res_plan_query(N * nl, 256, share, False, nt)
+
+
+def test_resident_byte_model_follows_the_variant():
+    """res_launch_bytes charges each variant what it moves: the w-only kernel 16 B
+    per unknown per pass (+ its streamed 2 %), the pairs kernels 8 B per unknown
+    whose running column sits in registers and 16 B per LDS-held unknown."""
+    n, p = _plan(4096)  # bench default: w-only, 126 of 128 chunks per workgroup on chip
+    assert p["variant"] == "w-only"
+    r = bench.res_regions(p, n)
+    assert sum(r.values()) == n and r["pairs"] == 0 and r["streamed"] / n < 0.02
+    per_pass = (bench.res_launch_bytes(p, n, 97) - bench.res_launch_bytes(p, n, 96)) / n
+    assert 16.0 < per_pass < 16.4
+    # 4096^2 / 2 and 8192^2 / 8 (k_mgs_res<12, 18> NT): 12 of 32 chunks pairs, 18 in LDS, 2 streamed
+    n, p = _plan(4096, 2)
+    assert p["variant"] == "pairs+lds"
+    r = bench.res_regions(p, n)
+    assert sum(r.values()) == n
+    assert r["pairs"] == 2 * 256 * 12 * 512 and r["w_on_chip"] == 2 * 256 * 18 * 512
+    per_pass = (bench.res_launch_bytes(p, n, 97) - bench.res_launch_bytes(p, n, 96)) / n
+    assert per_pass == pytest.approx(8 * 12 / 32 + 16 * 18 / 32 + 32 * 2 / 32, rel=1e-3)  # 14 B per unknown
+    # 4096^2 / 8 (k_mgs_res<8, 0>): everything pairs -> 8 B per unknown per pass
+    n, p = _plan(4096, 8)
+    assert p["variant"] == "pairs"
+    per_pass = (bench.res_launch_bytes(p, n, 97) - bench.res_launch_bytes(p, n, 96)) / n
+    assert per_pass == pytest.approx(8.0, rel=2e-3)
 
 
 def test_roofline_entry_is_a_fraction():
@@ -73,10 +110,18 @@ def test_roofline_entry_is_a_fraction():
     a = argparse.Namespace(m=95, method="mgsr", prof_every=16, grid=4096, prec="identity")
     prof = {k: (0.0, 0) for k in ["proj", "stencil", "scale", "update", "comm", "other"]}
     prof["res"] = (410.003, 100)
-    r = bench.roofline_entry(prof, a, 4096 * 4096, 20, 1)
-    assert 0.75 < r["frac"] < 0.85
+    n, p = _plan(4096)
+    r = bench.roofline_entry(prof, a, n, 20, 1, p)
+    # w-only: its reuse goes through the Infinity Cache -> the fabric read rate binds
+    assert r["bound"] == "fabric" and r["peak"] == bench.FABRIC_REF_GBPS and r["variant"] == "w-only"
+    assert 0.68 < r["frac"] < 0.78 and 0.74 < r["hbm_spec_frac"] < 0.84
+    assert 0.3 < r["hbm"]["frac"] < 0.5  # the DRAM side: about half the bytes
     assert r["alg_as_written_frac"] > 1.8
     assert r["avg_launch_us"] == pytest.approx(4100.03)
+    # a pairs+lds split (4096^2 on 2 GPUs): every byte from DRAM -> bound hbm
+    n2, p2 = _plan(4096, 2)
+    r2 = bench.roofline_entry(prof, a, n2, 20, 2, p2)
+    assert r2["bound"] == "hbm" and r2["peak"] == bench.HBM_PEAK_GBPS and r2["variant"] == "pairs+lds"
 
 
 def test_cpu_extrapolation_recovers_a_linear_step_cost():
@@ -148,3 +193,36 @@ def test_host_rhs_matches_the_oracle_on_slabs():
         parts = ga.slab_partition(N, R)
         b = np.concatenate([bench.rhs_ones_host(N, l0, nl) for l0, nl in parts])
         assert np.array_equal(b, ref)
+
+
+def _ctl_rank(rank, world, key, d, q):
+    from gmres_amd.ctl import Ctl
+
+    c = Ctl(rank, world, key=key, timeout=60, rdzv_dir=d)
+    out = {"all": c.allgather(rank * 10), "b": c.bcast("root" if rank == 0 else None),
+           "min": c.allreduce(rank + 1, "min"), "max": c.allreduce(rank + 0.5, "max"),
+           "sum": c.allreduce(rank, "sum")}
+    c.barrier()
+    c.close()
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_control_plane_world_size(world, tmp_path):
+    """bench.py's torch-free control plane (gmres_amd/ctl.py): rendezvous by a
+    file, gather / broadcast / min / max / sum identical on every rank."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ctl_rank, args=(r, world, "t", str(tmp_path), q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        o = got[r]
+        assert o["all"] == [10 * k for k in range(world)] and o["b"] == "root"
+        assert o["min"] == 1 and o["max"] == world - 0.5 and o["sum"] == world * (world - 1) // 2
+    assert not os.path.exists(os.path.join(str(tmp_path), "gk_ctl_t"))  # rank 0 removed the rendezvous file

@@ -86,14 +86,43 @@ def test_config5_4096_householder_vs_reference():
     _check_final_err(r, "hh_identity")
 
 
-@pytest.mark.parametrize("transport", ["local", "xchg"])
+@pytest.mark.parametrize("method,prec,key", [
+    ("mgsr", "identity", "mgsr_omp_identity_4096_m95_2cyc_t8"),
+    ("mgsr", "cbpr2", "mgsr_omp_cbpr2_4096_m95_2cyc_t8"),
+    ("hh", "identity", "hh_omp_identity_4096_m95_2cyc_t8"),
+])
+def test_4096_two_cycle_history_vs_reference(method, prec, key):
+    """The two restart cycles the bench legs time at 4096^2 (configs 1, 3's
+    cbpr2 leg, 5): both cycles' true residuals against the reference's own run
+    (oracle/_ref, 8 threads, tests/golden/make_ref_fixtures.py) at 1e-9."""
+    import gmres_amd as ga
+
+    g = REF[key]["hist_res"]
+    assert len(g) == 2
+    with ga.Context(4096, 95) as c:
+        c.set_precond(prec, (8.2, 0.2), 8)
+        c.set_rhs_ones()
+        if method == "mgsr":
+            r = ga.gmres_mgsr(c, 1e-15, max_cycles=2, want_verr=False, want_hist=True, want_x=False)
+        else:
+            r = ga.gmres_hh(c, 1e-15, precondition=False, max_cycles=2, want_verr=False, want_hist=True,
+                            want_x=False)
+    assert r.n_cycles == 2 and len(r.hist_res) >= 2
+    for a, b in zip(r.hist_res[:2], g):
+        assert a == pytest.approx(b, rel=1e-9), (r.hist_res[:2], g)
+
+
+@pytest.mark.parametrize("transport", ["local", "xchg", "xchg-res"])
 def test_config4_8192_eight_row_block_ranks_on_one_gpu(transport):
     """Config 4's decomposition (8 slabs of 1024 grid lines, per-projection
     all-reduce of the partial slabs, halo lines before every stencil) against a
     single-context 8192^2 run, through the in-process communicator (RCCL's
     message pattern) and through the device exchange the 8-GPU bench uses
     (tests/config4_run.py; a child process with GPU_MAX_HW_QUEUES=16 so that
-    the eight ranks' streams run concurrently).  The single-context run itself
+    the eight ranks' streams run concurrently) -- on the launch path, and
+    (xchg-res) with the resident step forced on, 32 workgroups per rank, so the
+    8 rank totals of every projection are summed inside the step launch.  The
+    single-context run itself
     is pinned to the reference's own 8192^2 cycle (tests/golden/make_ref_8192.py,
     the reference built from its sources, run on the GPU box's host).  Only the
     timing of config 4 needs 8 GPUs."""
@@ -104,13 +133,21 @@ def test_config4_8192_eight_row_block_ranks_on_one_gpu(transport):
         r = config4_run.run("local")
     else:
         env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
-        p = subprocess.run([sys.executable, "-u", os.path.join(HERE, "config4_run.py"), "xchg"], env=env,
+        p = subprocess.run([sys.executable, "-u", os.path.join(HERE, "config4_run.py"), transport], env=env,
                            capture_output=True, text=True, timeout=110)
         assert p.returncode == 0, p.stderr[-3000:]
         r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["ok"], r
     assert r["comm_kinds"] == (["local-group"] if transport == "local" else ["xgmi-device-exchange"]), r
     assert r["comm_launches"] > 0 and r["same_decisions"] and r["n_out"] == 95, r
+    if transport == "xchg-res":
+        # every Arnoldi step one resident launch per rank, no per-projection launch or
+        # all-reduce call: the only all-reduce launches left are the step's first dot
+        # (from the stencil's partial slab) and the cycle start's norm
+        assert r["res_G"] == [32] and r["res_launches_min"] >= 95 and r["proj_launches_max"] == 0, r
+        assert r["comm_launches_max"] <= 95 + 1, r
+    else:
+        assert r["res_launches_min"] == 0, r
     assert r["hist_res0"] == pytest.approx(r["ref_hist_res0"], rel=1e-9), r
     assert r["final_err_max_rel"] < 1e-6 and r["x_max_dev"] <= 1.0, r
     pin = REF.get("mgsr_omp_identity_8192_m95_1cyc_t16")

@@ -255,3 +255,76 @@ def test_chebyshev_uneven_slabs_bitexact(oracle, transport, degree):
         for c in ctxs:
             c.close()
         g.close()
+
+
+def _arnoldi_steps(c, nsteps):
+    """Cycle start + Arnoldi steps 1..nsteps through the C-ABI pieces: the H
+    columns and the local slab of V(:, nsteps + 1)."""
+    c.set_rhs_ones()
+    beta = c.mgs_cycle_start()
+    H = [c.mgs_step(j) for j in range(1, nsteps + 1)]
+    return beta, H, c.get_basis(nsteps)
+
+
+@pytest.mark.parametrize("transport", ["local", "xchg"])
+@pytest.mark.parametrize("split", ["even2", "even3", "thin"])
+@pytest.mark.parametrize("degree", [4, 8])
+def test_chebyshev_stencil_stage_on_slabs(transport, split, degree):
+    """The Arnoldi step's Chebyshev pass with the stencil as its stage 0
+    (GK_TUNE_CHEB_STEN, N >= 128) on row-block slabs: the pass takes k + 1
+    deep-halo lines of v (CF_HMAX, XS_HALO_LINES) and indexes the row + halo
+    offsets itself.  N = 130, Chebyshev(4) and (8), 2 and 3 ranks, through the
+    in-process group and the device exchange; 'thin' puts a slab of exactly k
+    lines between wide ones, so the k + 1 gate sends EVERY rank to the stencil
+    launch + pass route together.  Against one context: beta, the H columns of
+    steps 1..5 and V(:,6) (dot-product summation order only)."""
+    import gmres_amd as ga
+
+    N, m, steps = 130, 8, 5
+    with ga.Context(N, m) as c:
+        c.set_precond("cheb", (8.2, 0.2), degree)
+        b0, H0, v0 = _arnoldi_steps(c, steps)
+        assert c.res_info()["cheb_sten"] == 1
+    if split == "thin":
+        w = (N - degree) // 2
+        parts = [(0, w), (w, degree), (w + degree, N - w - degree)]
+    else:
+        parts = ga.slab_partition(N, 2 if split == "even2" else 3)
+    R = len(parts)
+    g = ga.LocalGroup(R)
+    ctxs = [ga.Context(N, m, device=0, line0=l0, nlines=nl) for l0, nl in parts]
+    out, err = [None] * R, []
+    try:
+        for q, c in enumerate(ctxs):
+            c.comm_init_local(g, q, max(nl for _, nl in parts))
+        if transport == "xchg":
+            for c in ctxs:
+                c.xchg_local()
+        for c in ctxs:
+            c.set_precond("cheb", (8.2, 0.2), degree)
+
+        def work(q):
+            try:
+                out[q] = _arnoldi_steps(ctxs[q], steps) + (ctxs[q].res_info()["cheb_sten"],)
+            except Exception as e:  # pragma: no cover - reported below
+                err.append(e)
+
+        th = [threading.Thread(target=work, args=(q,)) for q in range(R)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=100)
+        assert not err, err
+        # the stage-0 route on every rank, or (thin slab) on none
+        assert {o[3] for o in out} == ({0} if split == "thin" else {1}), [o[3] for o in out]
+        for o in out:  # replicated host values: identical on every rank
+            assert o[0] == out[0][0] and all(np.array_equal(a, b) for a, b in zip(o[1], out[0][1]))
+        assert out[0][0] == pytest.approx(b0, rel=1e-12)
+        for a, b in zip(out[0][1], H0):
+            assert np.allclose(a, b, rtol=1e-11, atol=1e-13 * np.abs(b).max()), (a, b)
+        v = np.concatenate([o[2] for o in out])
+        assert np.allclose(v, v0, rtol=1e-10, atol=1e-12 * np.abs(v0).max())
+    finally:
+        for c in ctxs:
+            c.close()
+        g.close()

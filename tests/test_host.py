@@ -4,6 +4,7 @@ loudly, the slab decomposition is sound."""
 import ctypes
 import os
 import subprocess
+import sys
 
 import pytest
 
@@ -113,3 +114,21 @@ def test_build_refuses_chebyshev_scratch_spills():
                "gk_api.hip:9:1: remark:     ScratchSize [bytes/lane]: 32 [-Rpass-analysis=kernel-resource-usage]\n")
     assert b._scratch_kernels(remarks, "k_cheb_fused") == ["_ZN2gk12k_cheb_fusedILi8ELb1ELb1ELi1ELb0EEEvNS_6CFArgsE"]
     assert [u[2] for u in b.HIP_UNITS] == ["gk_api.o"] + [f"gk_cheb{p}.o" for p in range(b.GK_CF_PARTS)]
+
+
+def test_torch_import_after_native_load_is_refused(built):
+    """The product never imports torch; once libgmres_hip.so runs on /opt/rocm's
+    HIP runtime in a torch-free process, importing torch (which would map its
+    bundled runtime as a second one and abort at exit) fails at the import."""
+    code = ("import gmres_amd._native as n; n.hip()\n"
+            "try:\n    import torch\n    print('IMPORTED')\n"
+            "except ImportError as e:\n    print('REFUSED', 'second one' in str(e))\n")
+    env = dict(os.environ)
+    env.pop("GK_TORCH_FIRST", None)
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.split() == ["REFUSED", "True"], p.stdout
+    # torch first, then the library: torch's runtime serves both (one runtime)
+    code2 = "import torch, gmres_amd._native as n; n.hip(); print('OK', 'torch' in n.runtime_paths().get('hip', 'torch'))"
+    p = subprocess.run([sys.executable, "-c", code2], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and p.stdout.split()[0] == "OK", (p.stdout, p.stderr[-2000:])

@@ -117,28 +117,26 @@ def _setup_worker(rank, world, port, mode, q):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
-    import torch.distributed as dist
-
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
+    from gmres_amd.ctl import Ctl
 
+    ctl = Ctl(rank, world, key=f"agree_{port}", timeout=120)
     c = _FakeCtx(rank, fail_open=(mode == "open" and rank == 1), fail_test=(mode == "test" and rank == 0))
     try:
-        out = bench.setup_xgmi(c, dist, world, rank, required=False)
+        out = bench.setup_xgmi(c, ctl, rank, required=False)
     except Exception as e:  # pragma: no cover
         out = repr(e)
     q.put((rank, out, c.enabled, c.opened))
-    dist.barrier()
-    dist.destroy_process_group()
+    ctl.barrier()
+    ctl.close()
 
 
 @pytest.mark.parametrize("mode", ["pass", "open", "test"])
 def test_bench_collective_agreement(mode):
     """bench.py --collective auto: the device exchange is used only if every
     rank mapped the regions and passed the self-test; otherwise every rank
-    switches it off and stays on RCCL (no rank may diverge)."""
+    switches it off and stays on RCCL (no rank may diverge).  The agreement runs
+    over bench.py's own control plane (gmres_amd/ctl.py), as in the bench."""
     world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

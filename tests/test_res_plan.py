@@ -39,13 +39,15 @@ def test_production_splits(N, R, variant, r2e, l2e, nt, hh):
         assert p["r2e"] == (90 if hh else 88)
 
 
+@pytest.mark.parametrize("R", [2, 4, 8])
 @pytest.mark.parametrize("N,prod", [(1448, (4096, 8)), (2048, (4096, 4)), (2896, (4096, 2)), (4096, (4096, 1))])
-def test_two_ranks_on_one_gpu_carry_the_production_load(N, prod):
-    """2 ranks x 128 workgroups on one GPU (the -m gpu split tests): the same
-    variant and the same chunks per workgroup as the production split on 256."""
-    t = _plan(N, 2, share=2)
+def test_ranks_on_one_gpu_carry_the_production_load(N, prod, R):
+    """R ranks x 256/R workgroups on one GPU (the -m gpu split tests): the same
+    variant and the same chunks per workgroup as the production split on 256
+    (the column load policy forced to the production split's, as the tests do)."""
     p = _plan(*prod)
-    assert t["G"] == 128 and p["G"] == 256
+    t = _plan(N, R, share=R, nt=p["nt"])
+    assert t["G"] == 256 // R and p["G"] == 256 and t["nt"] == p["nt"]
     for k in ("variant", "r2e", "l2e"):
         assert t[k] == p[k], (k, t, p)
     dt = 256 if p["variant"] == "w-only" else 512
