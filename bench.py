@@ -68,16 +68,20 @@ def mgs_step_bytes(n: int, j: int, model: str, sten: bool = False) -> float:
 
 def res_regions(plan: dict, nloc: int) -> dict:
     """How a resident launch holds the slab (gk_res_info): unknowns whose w AND
-    running Krylov column sit in registers ("pairs": the pairs / prefetch
-    variants), unknowns whose w alone is on chip (registers of the w-only
-    variant, or LDS), and the streamed rest.  Chunks of DT double2: 256 (w-only),
-    448 (prefetch, one control wave), 512 (pairs)."""
+    running Krylov column sit on chip ("pairs": the pairs / prefetch variants,
+    and the w+column variant's cached chunks), unknowns whose w alone is on chip
+    (registers of the w-only variant, or LDS), and the streamed rest.  Chunks of
+    DT double2: 256 (w-only, w+column), 448 (prefetch, one control wave), 512
+    (pairs)."""
     n2 = nloc // 2
-    dt = 256 if plan["variant"] == "w-only" else (448 if plan.get("cw") else 512)
+    dt = 256 if plan["variant"] in ("w-only", "w+column") else (448 if plan.get("cw") else 512)
     nres2 = min(int(plan["nres2"]), n2)
     nreg2 = min(nres2, int(plan["G"]) * int(plan["r2e"]) * dt)
     if plan["variant"] == "w-only":
         return {"pairs": 0, "w_on_chip": 2 * nres2, "streamed": 2 * (n2 - nres2) + (nloc & 1)}
+    if plan["variant"] == "w+column":  # w in registers; the column of r2 + l2 chunks per thread cached
+        cached = min(nres2, int(plan["G"]) * min(int(plan["r2e"]), int(plan["r2"]) + int(plan["l2"])) * dt)
+        return {"pairs": 2 * cached, "w_on_chip": 2 * (nres2 - cached), "streamed": 2 * (n2 - nres2) + (nloc & 1)}
     return {"pairs": 2 * nreg2, "w_on_chip": 2 * (nres2 - nreg2), "streamed": 2 * (n2 - nres2) + (nloc & 1)}
 
 
@@ -369,17 +373,24 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: d
     m = args.m
     on_res = bool(prof) and prof.get("res", (0.0, 0))[1] > 0 and plan is not None and plan.get("variant")
     if not on_res:
-        if not prof or prof["proj"][1] == 0:
+        if not prof or (prof["proj"][1] == 0 and prof.get("graph", (0.0, 0))[1] == 0):
             return None
         # launch-per-projection path (RCCL multi-rank, or after a fallback)
-        ms, launches = prof["proj"]
         S = 1 if args.method == "hh" else max(1, args.prof_every)
         steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
         nproj = sum(2 * j for j in steps_js)
         fused, written = 32.0 * nloc * nproj, 40.0 * nloc * nproj
-        kname = "gk::k_proj (AXPY_i fused with dot_{i+1}, one launch per projection)"
-        timing = f"HIP events around every projection launch of steps j % {S} == 0 of the timed cycles"
-        per_proj = ms * 1e3 / launches
+        if prof.get("graph", (0.0, 0))[1] > 0 and args.method == "mgsr":  # the step replayed as a hipGraph
+            ms, launches = prof["graph"]
+            fused += sum(16.0 * nloc for _ in steps_js)  # + the normalisation (w in, V(:,j+1) out)
+            kname = ("hipGraph of a launch-path MGS-R step (2j gk::k_proj launches with their 2j + 1 all-reduces "
+                     "and k_scale, captured once per j, GK_TUNE_GRAPH)")
+            timing = f"HIP events around every replayed step graph of steps j % {S} == 0 of the timed cycles"
+        else:
+            ms, launches = prof["proj"]
+            kname = "gk::k_proj (AXPY_i fused with dot_{i+1}, one launch per projection)"
+            timing = f"HIP events around every projection launch of steps j % {S} == 0 of the timed cycles"
+        per_proj = ms * 1e3 / nproj
         variant, regions, bound, peak = "launch-per-projection", None, "hbm", HBM_PEAK_GBPS
         model = "32 B per unknown per projection (w read + written, both Krylov columns)"
     else:

@@ -157,6 +157,12 @@ struct gk_ctx {
     int tune_cheb_sten = 1;   // the Arnoldi step's pass forms z = A v itself (stage 0)
     int tune_res_sten = 0;    // the w-only MGS step launch forms w = A V(:,j) itself (A/B: slower)
     int tune_spin_wait = 1;   // the per-step host wait spins on its event (0: hipEventSynchronize)
+    int tune_graph = 1;       // launch-path MGS-R steps captured as hipGraphs (RCCL / no collective)
+    int tune_res_qdef = -1;   // k_mgs_res NT: V_q of the LDS / streamed parts with the default policy (-1 auto)
+    int tune_res_pc = -1;     // column-cache variant k_mgs_wpc: -1 by the byte model, 0 never, 1 where it fits
+    std::vector<hipGraphExec_t> gstep;  // captured step j (launch path), valid for partial-slab count gkey
+    int gkey = -1;
+    bool capturing = false;   // a step is being captured: no profiling events inside it
     // tuning knobs (gk_set_tuning)
     int tune_nt = -1, tune_pj_blocks = 0, tune_st_blocks = 0;  // tune_nt: -1 auto
     bool nt_auto = false;
@@ -195,7 +201,7 @@ struct ProfScope {
     gk_ctx *c;
     int slot = -1;
     ProfScope(gk_ctx *c_, int kid) : c(c_) {
-        if (!c->prof || !c->prof_on_step) return;
+        if (!c->prof || !c->prof_on_step || c->capturing) return;
         if (c->nev == PROF_POOL) prof_harvest(c);
         slot = c->nev++;
         c->evk[slot] = kid;
@@ -207,6 +213,18 @@ struct ProfScope {
 };
 
 double *slot(gk_ctx *c, int s) { return c->red + (i64)s * gk::NPMAX; }
+
+// Captured launch-path steps hold kernel arguments and communicator calls of the
+// configuration they were captured in: any change of tuning, preconditioner or
+// communicator drops them.
+void graph_reset(gk_ctx *c) {
+    for (hipGraphExec_t &g : c->gstep)
+        if (g != nullptr) {
+            (void)hipGraphExecDestroy(g);
+            g = nullptr;
+        }
+    c->gkey = -1;
+}
 
 // ----------------------------------------------------------------- comm ---
 constexpr int LG_MAX = 16;
@@ -643,21 +661,45 @@ struct ResPlan {
     int G = 0, r2 = 0, l2 = 0;
     int r2e = 0, l2e = 0;  // chunks per workgroup used: the resident prefix spread evenly over G
     bool pf = false, nt = false, cw = false, wo = false;
+    bool pc = false;       // column-cache variant (k_mgs_wpc): w in registers, running column cached
     i64 nres2 = 0;
     int lds = 0;
 };
 
+// Column-cache variant (k_mgs_wpc): w of up to RES_PC_RW chunks per thread in
+// registers, the running column of RES_PC_RX of them in registers and of
+// RES_PC_LX in LDS (26 + 38 = all 64: the slab of one GPU of 4096^2 / 2 and of
+// 8192^2 / 8).
+constexpr int RES_PC_RW = 64, RES_PC_RX = 26, RES_PC_LX = 38;
+
+// Modelled bytes per projection of a slab of n2 double2 on G workgroups (the
+// unit of pairs_bytes / wonly_bytes: 8 per double2 whose w and running column are
+// on chip, 16 per double2 of w alone, 32 per streamed double2) under the
+// column-cache variant: the cached pairs, the rest of the register-held w, the
+// streamed rest.
+i64 pc_bytes(i64 n2, int G) {
+    const i64 cap = (i64)G * RES_PC_RW * gk::WT, cached = (i64)G * (RES_PC_RX + RES_PC_LX) * gk::WT;
+    const i64 r = std::min(n2, cap), c = std::min(r, cached);
+    return 8 * c + 16 * (r - c) + 32 * (n2 - r);
+}
+
 // Modelled fabric bytes per projection (per double2) of the two large-slab
 // variants: pairs (w + running column, 8 B/unknown) in 2 x 12 registers + w in
 // LDS (16 B) vs w only in registers + LDS (16 B); the rest streams (32 B).
-bool wonly_pays(i64 n2, int G) {
+i64 pairs_bytes(i64 n2, int G) {  // k_mgs_res<12, 18>: 2 x 12 registers + 18 LDS chunks of w
     const i64 rp = (i64)G * RES_R2_BIG * gk::RT, lp = (i64)G * RES_L2 * gk::RT;
-    const i64 rw = (i64)G * (RES_RW + RES_LW) * gk::WT;
     auto clamp = [](i64 v) { return v < 0 ? (i64)0 : v; };
     const i64 pr = std::min(n2, rp), pl = std::min(clamp(n2 - rp), lp), ps = clamp(n2 - rp - lp);
-    const i64 wr = std::min(n2, rw), ws = clamp(n2 - rw);
-    return 16 * wr + 32 * ws < 8 * pr + 16 * pl + 32 * ps;
+    return 8 * pr + 16 * pl + 32 * ps;
 }
+
+i64 wonly_bytes(i64 n2, int G) {
+    const i64 rw = (i64)G * (RES_RW + RES_LW) * gk::WT;
+    const i64 wr = std::min(n2, rw), ws = n2 > rw ? n2 - rw : 0;
+    return 16 * wr + 32 * ws;
+}
+
+bool wonly_pays(i64 n2, int G) { return wonly_bytes(n2, G) < pairs_bytes(n2, G); }
 
 // The variant a slab of nloc local unknowns runs on (pure: no context, no
 // device; gk_res_plan_query exposes it so the CPU tests pin what every
@@ -667,7 +709,8 @@ bool wonly_pays(i64 n2, int G) {
 //   else w only in registers + LDS when the byte model says so (GK_TUNE_RES_WONLY);
 //   else w and the running column in 2 x 12 registers, plus (GK_TUNE_RES_LDS)
 //   w of 18 more chunks per workgroup in LDS, the rest streamed.
-void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bool hh, bool nt, ResPlan &p) {
+void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bool hh, bool nt, ResPlan &p,
+                   int tune_pc = -1) {
     const i64 n2 = nloc / 2;
     const i64 dcw = gk::RT - 64;
     // small vectors: no more workgroups than two chunks each (a cheaper all-gather)
@@ -689,10 +732,24 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         p.l2e = (int)std::min<i64>(lmax, (rest + G - 1) / G);
         p.nres2 = std::min<i64>(nchf, G * (p.r2e + p.l2e)) * dt;
     };
+    // the column-cache variant where it moves fewer bytes than both large-slab
+    // variants (strictly: a tie keeps the older kernel)
+    const bool pc_fits = n2 <= (i64)gmax * RES_PC_RW * gk::WT;
+    const bool pc_pays = pc_fits && pc_bytes(n2, gmax) < std::min(pairs_bytes(n2, gmax), wonly_bytes(n2, gmax));
     if (p.r2 >= need || cap < RES_R2_BIG) {
         p.G = gcw;
         p.pf = p.cw = true;
         spread(dcw, p.r2, 0);
+    } else if (tune_wonly <= 0 && (tune_pc > 0 ? pc_fits : (tune_pc < 0 && pc_pays))) {
+        // w wholly in registers, the running column cached (k_mgs_wpc): 8 B/unknown
+        p.G = gmax;
+        p.pc = true;
+        p.r2 = RES_PC_RX;
+        p.l2 = RES_PC_LX;
+        spread(gk::WT, RES_PC_RW, 0);
+        p.lds = RES_PC_LX * gk::WT * (int)sizeof(double2);
+        p.nt = true;
+        return;
     } else if (tune_wonly > 0 || (tune_wonly < 0 && wonly_pays(n2, gmax))) {
         // w only, one wave per SIMD: 16 B/unknown per projection for ~100 chunks per workgroup
         p.G = gmax;
@@ -731,7 +788,7 @@ bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
     const int gmax = std::max(1, std::min(gk::RGMAX, c->res_cus / std::max(1, c->res_share)));
     const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : RES_R2_BIG;
     plan_resident(c->nloc, gmax, cap, c->tune_res_lds, c->tune_res_wonly, hh,
-                  c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p);
+                  c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p, c->tune_res_pc);
     return true;
 }
 
@@ -741,7 +798,8 @@ enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, R
 void plan_info(const ResPlan &p, bool on, long long *info) {
     for (int k = 0; k < GK_RES_INFO_LEN; ++k) info[k] = 0;
     if (!on) return;
-    info[RPI_VARIANT] = p.wo ? GK_RES_WONLY : (p.pf ? GK_RES_PREFETCH : (p.l2 > 0 ? GK_RES_PAIRS_LDS : GK_RES_PAIRS));
+    info[RPI_VARIANT] = p.pc ? GK_RES_WCOL
+                             : (p.wo ? GK_RES_WONLY : (p.pf ? GK_RES_PREFETCH : (p.l2 > 0 ? GK_RES_PAIRS_LDS : GK_RES_PAIRS)));
     info[RPI_G] = p.G;
     info[RPI_R2] = p.r2;
     info[RPI_L2] = p.l2;
@@ -807,8 +865,29 @@ int launch_wres(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     }
 }
 
+template <int MODE>
+int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    static std::atomic<int> attr[ATTR_DEVS];
+    if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
+    if (attr[c->dev].load() < p.lds) {
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
+        attr[c->dev] = p.lds;
+    }
+    gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE><<<p.G, gk::WT, p.lds, c->st>>>(a);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
 int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     if (p.wo) return launch_wres(c, p, a);
+    if (p.pc) {
+        switch (a.mode) {
+            case gk::RES_HH_UP: return launch_wpc_m<gk::RES_HH_UP>(c, p, a);
+            case gk::RES_HH_DOWN: return launch_wpc_m<gk::RES_HH_DOWN>(c, p, a);
+            default: return launch_wpc_m<gk::RES_MGS>(c, p, a);
+        }
+    }
 #define GK_RES_CASE(R, L, PFV, CWV)                                                                 \
     if (p.r2 == R && p.l2 == L && p.pf == PFV && p.cw == CWV)                                      \
         return p.nt ? launch_res_t<R, L, PFV, true, CWV>(c, p, a) : launch_res_t<R, L, PFV, false, CWV>(c, p, a);
@@ -880,6 +959,9 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
         c->res_trace_np = np;
     }
     a.sten_v = sten_v;
+    // auto: on -- A/B at 2896^2 (k_mgs_res<12, 18> NT, profiles/r04/ab_qdef_2896_r04a.jsonl): 19.98 /
+    // 19.90 -> 18.82 / 18.84 us per projection
+    a.qdef = c->tune_res_qdef != 0 ? 1 : 0;
     a.slo = halo_lo(c);
     a.shi = halo_hi(c);
     a.N = c->N;
@@ -1272,6 +1354,64 @@ int reflect_chain_down(gk_ctx *c, double *v, int k, i64 unit_g = -1, int flags =
     return GK_OK;
 }
 
+// The launch path's MGS-R cascade of step j after the operator launch left the
+// first dot's partial slab (np partials) in slot 0: two passes of j projections
+// (AXPY_i fused with dot_{i+1}), each dot all-reduced, then h = ||w|| and
+// V(:,j+1) = w / h with H(1:j+1, j) published to mapped host memory.
+// gmres_mgsr.f90:341-363, :384.
+int mgs_chain(gk_ctx *c, int j, int np) {
+    const i64 ld = c->ld;
+    double *V = c->V;
+    const int m2 = c->m + 2;
+    double *hs = c->hall + (i64)(j - 1) * m2;
+    int s0 = 0, s1 = 1;
+    const int np_total = 2 * j;
+    for (int p = 0; p < np_total; ++p) {
+        const int i = p % j;
+        CHK(allreduce(c, slot(c, s0), np));
+        const double *va = V + (i64)i * ld;
+        const int first_pass = p < j;
+        if (p + 1 < np_total) {
+            const double *vb = V + (i64)((p + 1) % j) * ld;
+            CHK(proj(c, gk::PJ_AXPY_DOT, c->w, va, vb, slot(c, s0), np, slot(c, s1), hs + i, 1.0, 0, first_pass));
+        } else {
+            CHK(proj(c, gk::PJ_AXPY_NORM, c->w, va, nullptr, slot(c, s0), np, slot(c, s1), hs + i, 1.0, 0,
+                     first_pass));
+        }
+        np = c->np_pj;
+        std::swap(s0, s1);
+    }
+    CHK(allreduce(c, slot(c, s0), np));
+    return scale(c, V + (i64)j * ld, c->w, slot(c, s0), np, hs + j, c->hallh_dev + (i64)(j - 1) * m2, hs, j);
+}
+
+// Capture mgs_chain(j) once as a graph (its kernel arguments and communicator
+// calls depend only on j, np and the context's fixed buffers).  A capture that
+// fails switches graphs off for this context; the step then runs call by call.
+int capture_step(gk_ctx *c, int j, int np) {
+    HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+    c->capturing = true;
+    const int rc = mgs_chain(c, j, np);
+    c->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(c->st, &g);
+    hipGraphExec_t ge = nullptr;
+    hipError_t e2 = hipErrorUnknown;
+    if (rc == GK_OK && e == hipSuccess && g != nullptr) e2 = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    if (g != nullptr) (void)hipGraphDestroy(g);
+    if (rc != GK_OK || e != hipSuccess || e2 != hipSuccess) {
+        const std::string why = rc != GK_OK ? g_err : hipGetErrorString(e != hipSuccess ? e : e2);
+        (void)hipGetLastError();
+        c->tune_graph = 0;
+        graph_reset(c);
+        set_err(GK_OK, "launch-path step graphs off for this context: capture of step %d failed (%s)", j,
+                why.c_str());
+        return GK_OK;
+    }
+    c->gstep[j] = ge;
+    return GK_OK;
+}
+
 }  // namespace
 
 // ======================================================================= API
@@ -1378,6 +1518,7 @@ int gk_destroy(gk_ctx *c) {
     if (c == nullptr) return GK_OK;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
+    graph_reset(c);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->lev_a) (void)hipEventDestroy(c->lev_a);
     if (c->lev_b) (void)hipEventDestroy(c->lev_b);
@@ -1419,6 +1560,7 @@ int gk_comm_unique_id(unsigned char id[128]) {
 int gk_comm_init(gk_ctx *c, int nranks, int rank, int max_lines, const unsigned char id[128]) {
     if (c == nullptr || nranks < 1 || rank < 0 || rank >= nranks || max_lines < c->nlines)
         return set_err(GK_ERR_ARG, "bad comm args");
+    graph_reset(c);
     HIPCHK(hipSetDevice(c->dev));
     c->nranks = nranks;
     c->rank = rank;
@@ -1457,6 +1599,7 @@ int gk_group_destroy(gk_group *g) {
 int gk_comm_init_local(gk_ctx *c, gk_group *g, int rank, int max_lines) {
     if (c == nullptr || g == nullptr || rank < 0 || rank >= g->n || max_lines < c->nlines)
         return set_err(GK_ERR_ARG, "bad local comm args");
+    graph_reset(c);
     HIPCHK(hipSetDevice(c->dev));
     c->nranks = g->n;
     c->rank = rank;
@@ -1481,6 +1624,7 @@ int gk_comm_init_local(gk_ctx *c, gk_group *g, int rank, int max_lines) {
 int gk_comm_init_xgmi(gk_ctx *c, int nranks, int rank, int max_lines) {
     if (c == nullptr || nranks < 1 || nranks > gk::XS_MAXR || rank < 0 || rank >= nranks || max_lines < c->nlines)
         return set_err(GK_ERR_ARG, "bad xgmi comm args (nranks <= %d)", gk::XS_MAXR);
+    graph_reset(c);
     HIPCHK(hipSetDevice(c->dev));
     if (c->comm != nullptr) {  // an RCCL communicator of an abandoned gk_comm_init: the exchange replaces it
         // abort, not destroy: ncclCommDestroy finalises collectively and can wait on
@@ -1570,6 +1714,7 @@ int gk_xchg_local(gk_ctx *c) {
 
 int gk_xchg_enable(gk_ctx *c, int on) {
     if (c == nullptr) return set_err(GK_ERR_ARG, "null context");
+    graph_reset(c);
     if (on && !c->xs_ready) return set_err(GK_ERR_STATE, "exchange not open");
     if (on && c->xs_broken)
         return set_err(GK_ERR_STATE, "device exchange retired after a missed deadline (sequence numbers may "
@@ -1729,6 +1874,7 @@ int gk_set_precond(gk_ctx *c, int kind, const double *params, int nparams, int d
         c->p1 = params[1];
     }
     c->pdeg = degree;
+    graph_reset(c);
     if (kind == GK_PREC_CHEB && std::fabs(c->p1 - c->p0) == 0.0)
         return set_err(GK_ERR_ARG, "Chebyshev interval is empty");
     return GK_OK;
@@ -1849,7 +1995,7 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
     const int m2 = c->m + 2;
     double *hs = c->hall + (i64)(j - 1) * m2;  // H(1:j+1, j) of this step, on device
     c->prof_on_step = (j % c->prof_every) == 0;
-    int s0 = 0, s1 = 1;
+    const int s0 = 0;
     ResPlan rp;
     const bool res = res_plan(c, rp);
     if (res && res_sten(c, rp)) {  // w = A V(:,j), the first dot and the cascade: ONE launch
@@ -1870,26 +2016,26 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
         c->prof_on_step = true;
         return GK_OK;
     }
-    // two MGS passes: projection p = (k, i), AXPY of p fused with the dot of p+1
-    const int np_total = 2 * j;
-    for (int p = 0; p < np_total; ++p) {
-        const int i = p % j;
-        CHK(allreduce(c, slot(c, s0), np));
-        const double *va = V + (i64)i * ld;
-        const int first_pass = p < j;
-        if (p + 1 < np_total) {
-            const double *vb = V + (i64)((p + 1) % j) * ld;
-            CHK(proj(c, gk::PJ_AXPY_DOT, c->w, va, vb, slot(c, s0), np, slot(c, s1), hs + i, 1.0, 0, first_pass));
-        } else {
-            CHK(proj(c, gk::PJ_AXPY_NORM, c->w, va, nullptr, slot(c, s0), np, slot(c, s1), hs + i, 1.0, 0,
-                     first_pass));
+    // Launch path: RCCL ranks (or one rank with the resident step off) replay the
+    // step's projection chain as a hipGraph captured at its first use (GK_TUNE_GRAPH).
+    if (c->tune_graph && !c->tune_rev && !c->xs_on && c->lg == nullptr) {
+        if (c->gkey != np) {
+            graph_reset(c);
+            c->gkey = np;
         }
-        np = c->np_pj;
-        std::swap(s0, s1);
+        if ((int)c->gstep.size() < c->m + 1) c->gstep.resize(c->m + 1, nullptr);
+        if (c->gstep[j] == nullptr) CHK(capture_step(c, j, np));
+        if (c->gstep[j] != nullptr) {
+            {
+                ProfScope ps(c, GK_KID_GRAPH);
+                HIPCHK(hipGraphLaunch(c->gstep[j], c->st));
+            }
+            HIPCHK(hipEventRecord(c->ev_step[j], c->st));
+            c->prof_on_step = true;
+            return GK_OK;
+        }
     }
-    CHK(allreduce(c, slot(c, s0), np));
-    // h = ||w||, V(:,j+1) = w / h; H(1:j+1,j) published to mapped host memory
-    CHK(scale(c, V + (i64)j * ld, c->w, slot(c, s0), np, hs + j, c->hallh_dev + (i64)(j - 1) * m2, hs, j));
+    CHK(mgs_chain(c, j, np));
     HIPCHK(hipEventRecord(c->ev_step[j], c->st));
     c->prof_on_step = true;
     return GK_OK;
@@ -2229,6 +2375,9 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_CHEB_STEN: c->tune_cheb_sten = value != 0; break;
         case GK_TUNE_RES_STEN: c->tune_res_sten = value != 0; break;
         case GK_TUNE_SPIN_WAIT: c->tune_spin_wait = value != 0; break;
+        case GK_TUNE_GRAPH: c->tune_graph = value != 0; break;
+        case GK_TUNE_RES_QDEF: c->tune_res_qdef = value < 0 ? -1 : (value != 0); break;
+        case GK_TUNE_RES_PC: c->tune_res_pc = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_VERR_ORDER: c->tune_verr_order = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
@@ -2242,6 +2391,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         default: return set_err(GK_ERR_ARG, "unknown tuning key %d", key);
     }
     set_geometry(c);
+    graph_reset(c);
     return GK_OK;
 }
 

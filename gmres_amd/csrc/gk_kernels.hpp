@@ -897,6 +897,10 @@ struct ResArgs {
     const double *sten_v;         // V(:,j)
     const double *slo, *shi;      // its halo lines -1 / nlines (nullptr: the physical boundary)
     int N, nlines;                // grid side, slab lines
+    // k_mgs_res with NT: the LDS-held and streamed parts load their dot column V_q
+    // with the default policy (it is the next pass's AXPY column V_i: then an
+    // Infinity-Cache hit), V_i non-temporal -- the w-only kernel's policy
+    int qdef;
 };
 constexpr int RES_TRACE_X = 2 * RHMAX + 2;  // exchanges recorded per workgroup (all of one launch)
 
@@ -1378,7 +1382,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                         if (k + u < L2 && c < lend) {
                             wv[u] = lw[(k + u) * DT + td];
                             av[u] = ldv<NT>(A2 + c * DT + td);
-                            if (!last) bv[u] = ldv<NT>(B2 + c * DT + td);
+                            if (!last) bv[u] = a.qdef ? ldv<false>(B2 + c * DT + td) : ldv<NT>(B2 + c * DT + td);
                         }
                     }
 #pragma unroll
@@ -1407,7 +1411,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                     if (e < n2) {
                         wv[u] = W2[e];
                         av[u] = ldv<NT>(A2 + e);
-                        if (!last) bv[u] = ldv<NT>(B2 + e);
+                        if (!last) bv[u] = a.qdef ? ldv<false>(B2 + e) : ldv<NT>(B2 + e);
                     }
                 }
 #pragma unroll
@@ -1997,6 +2001,212 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     clk.finish(a.stamps, mode);
     if (mode == RES_MGS && blockIdx.x == 0) {
+        __syncthreads();
+        for (int k = t; k < j; k += WT) {
+            a.hs[k] = hsh[k];
+            a.hcopy[k] = hsh[k];
+        }
+        if (t == 0) {
+            a.hs[j] = hn;
+            a.hcopy[j] = hn;
+        }
+    }
+}
+
+
+// --------------------------------------------------------------------------
+// Resident MGS-R step, column-cache variant (k_mgs_wres's structure: ONE wave
+// per SIMD, 256-thread workgroups, one per CU): w wholly in registers (RW
+// double2 per thread) and the running Krylov column cached on chip -- RX
+// double2 per thread in registers, LX more in LDS.  A pass reads only its dot
+// column V_q (its AXPY column V_i is the previous pass's V_q, still cached):
+// 8 B per unknown per projection, against 16 B for the w-only kernel and for
+// k_mgs_res's LDS-held w.  For slabs of up to RW chunks per thread -- the slab
+// of one GPU of 4096^2 / 2 and of 8192^2 / 8 is 64 (RX + LX = 62 cached), of
+// 4096^2 / 4 is 32.  Chunks past RX + LX (not cached) read V_i too (16 B),
+// chunks past RW stream (32 B).  Same exchange, same element arithmetic as
+// k_mgs_res / k_mgs_wres; only the dot summation order within a thread
+// differs.  Columns non-temporal (nothing is re-read through the caches).
+// --------------------------------------------------------------------------
+template <int RW, int RX, int LX, int MODE, int WBT = 8>
+__global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
+    static_assert(RX <= RW && RX + LX <= RW, "the column cache covers register chunks of w only");
+    extern __shared__ double2 lx[];  // [LX][WT]: cached column of chunks RX .. RX + LX - 1
+    __shared__ double sm[WT / 64];
+    __shared__ double bc[1];
+    __shared__ int okf;
+    __shared__ double hsh[RHMAX + 1];
+    const int t = threadIdx.x;
+    constexpr int mode = MODE;
+    const int j = a.j, np = res_np(mode, j);
+    const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
+    const i64 nch = a.nres2 / WT;
+    const i64 c0 = (i64)blockIdx.x * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
+    const i64 tail0 = mode == RES_HH_UP ? a.tail0 : 0;
+    const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
+    double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
+    ResClock clk;
+    clk.start(a.stamps);
+    const i64 sstride = (i64)gridDim.x * WT;
+    const i64 sbase = a.nres2 + (i64)blockIdx.x * WT + t;
+    double2 wr[RW], xc[RX > 0 ? RX : 1];
+    {  // w, and the AXPY column of pass 0 into the cache
+        const double2 *__restrict__ C2 = V2 + (i64)res_col(mode, j, 0) * ld2;
+#pragma unroll
+        for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < RX; ++k) xc[k] = (c0 + k < cend) ? ldv<true>(C2 + (c0 + k) * WT + t) : double2{0.0, 0.0};
+        for (int k = 0; k < LX; ++k)
+            if (c0 + RX + k < cend) lx[k * WT + t] = ldv<true>(C2 + (c0 + RX + k) * WT + t);
+    }
+    // One pass: w -= ch V_i (the cached column; V_i from HBM past the cache), then
+    // the reduction `kind`; with a dot, V_q replaces the cached column.
+    auto pass = [&](double ch, int i, int q, int kind) -> double {
+        const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
+        const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
+        const bool dot = kind == RK_DOT;
+        double acc = 0.0;
+#pragma unroll
+        for (int k0 = 0; k0 < RW; k0 += WBT) {
+            double2 av[WBT], bv[WBT];
+#pragma unroll
+            for (int u = 0; u < WBT; ++u) {
+                const int k = k0 + u;
+                const i64 c = c0 + k;
+                if (k < RW && c < cend) {
+                    if (dot) bv[u] = ldv<true>(B2 + c * WT + t);
+                    if (k >= RX + LX) av[u] = ldv<true>(A2 + c * WT + t);  // not cached
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < WBT; ++u) {
+                const int k = k0 + u;
+                if (k < RW && c0 + k < cend) {
+                    double2 x;
+                    if (k < RX)
+                        x = xc[k < RX ? k : 0];
+                    else if (k < RX + LX)
+                        x = lx[(k - RX) * WT + t];
+                    else
+                        x = av[u];
+                    wr[k].x = wr[k].x - ch * x.x;
+                    wr[k].y = wr[k].y - ch * x.y;
+                    if (dot) {
+                        acc = acc + wr[k].x * bv[u].x;
+                        acc = acc + wr[k].y * bv[u].y;
+                        if (k < RX)
+                            xc[k < RX ? k : 0] = bv[u];
+                        else if (k < RX + LX)
+                            lx[(k - RX) * WT + t] = bv[u];
+                    } else if (kind == RK_NORM) {
+                        sq_acc(acc, wr[k], (c0 + k) * WT + t, tail0, mode == RES_HH_UP && c0 + k == 0);
+                    }
+                }
+            }
+        }
+        for (i64 e0 = sbase; e0 < n2; e0 += 2 * sstride) {  // streamed part: 32 B/unknown
+            double2 wv[2], av[2], bv[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const i64 e = e0 + u * sstride;
+                if (e < n2) {
+                    wv[u] = W2[e];
+                    av[u] = ldv<true>(A2 + e);
+                    if (dot) bv[u] = ldv<true>(B2 + e);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const i64 e = e0 + u * sstride;
+                if (e < n2) {
+                    wv[u].x = wv[u].x - ch * av[u].x;
+                    wv[u].y = wv[u].y - ch * av[u].y;
+                    W2[e] = wv[u];
+                    if (dot) {
+                        acc = acc + wv[u].x * bv[u].x;
+                        acc = acc + wv[u].y * bv[u].y;
+                    } else if (kind == RK_NORM) {
+                        sq_acc(acc, wv[u], e, tail0, mode == RES_HH_UP && 2 * a.nres2 < tail0);
+                    }
+                }
+            }
+        }
+        if ((a.n & 1) && blockIdx.x == 0 && t == 0) {  // odd-length tail element
+            const i64 e = a.n - 1;
+            const double x = a.w[e] - ch * a.V[(i64)i * a.ld + e];
+            a.w[e] = x;
+            if (dot) acc = acc + x * a.V[(i64)q * a.ld + e];
+            if (kind == RK_NORM && e >= tail0) acc = acc + x * x;
+        }
+        return acc;
+    };
+    int xi = 0;
+    auto reduce = [&](double acc, double &h) -> bool {
+        clk.passed(a.stamps);
+        acc = wave_sum(acc);
+        if ((t & 63) == 0) sm[t >> 6] = acc;
+        __syncthreads();
+        if (t < 64) res_exchange<WT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
+        __syncthreads();
+        ++xi;
+        h = bc[0];
+        clk.waited(a.stamps);
+        return okf != 0;
+    };
+    auto kind_of = [&](int p) { return p < np - 1 ? RK_DOT : (mode == RES_HH_DOWN ? RK_NONE : RK_NORM); };
+    double h;
+    bool ok = true;
+    if (mode == RES_HH_DOWN) {
+        // the pre-dot <v, V_col(0)> as a pass with h = 0 (w - 0 V = w; the cache is
+        // refilled with the same column)
+        const int q = res_col(mode, j, 0);
+        double acc = 0.0;
+        if (a.unit_known) {  // <e_u, P_q> = P_q(u): the one nonzero product, as the full sum gives it
+            if (blockIdx.x == 0 && t == 0 && a.unit_e >= 0) acc = a.V[(i64)q * a.ld + a.unit_e];
+        } else {
+            acc = pass(0.0, q, q, RK_DOT);
+        }
+        ok = reduce(acc, h);
+    } else {
+        double s = 0.0;
+        for (int k = t; k < a.npin; k += WT) s += a.pin[k];
+        s = wave_sum(s);
+        if ((t & 63) == 0) sm[t >> 6] = s;
+        __syncthreads();
+        h = sm[0];
+#pragma unroll
+        for (int w = 1; w < WT / 64; ++w) h += sm[w];
+        __syncthreads();
+    }
+    for (int p = 0; p < np && ok; ++p) {
+        const int i = res_col(mode, j, p);
+        const int kind = kind_of(p);
+        if (mode == RES_MGS && blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
+        const double acc = pass(mode == RES_MGS ? h : a.coef * h, i, res_col(mode, j, p + 1), kind);
+        if (kind != RK_NONE) ok = reduce(acc, h);
+    }
+    if (!ok) return;  // uniform per workgroup; *err is set
+    if (mode != RES_MGS) {  // reflections: w back to HBM (RES_HH_UP: h = ||w(j+1:n)||^2)
+#pragma unroll
+        for (int k = 0; k < RW; ++k)
+            if (c0 + k < cend) W2[(c0 + k) * WT + t] = wr[k];
+        if (mode == RES_HH_UP && blockIdx.x == 0 && t == 0) a.hs[0] = h;
+        clk.finish(a.stamps, mode);
+        return;
+    }
+    const double hn = sqrt(h);
+    double2 *__restrict__ O2 = reinterpret_cast<double2 *>(a.vout);
+#pragma unroll
+    for (int k = 0; k < RW; ++k)
+        if (c0 + k < cend)
+            O2[(c0 + k) * WT + t] = hn != 0.0 ? double2{wr[k].x / hn, wr[k].y / hn} : double2{0.0, 0.0};
+    for (i64 e = sbase; e < n2; e += sstride) {
+        const double2 v = W2[e];
+        O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
+    }
+    if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
+    clk.finish(a.stamps, mode);
+    if (blockIdx.x == 0) {
         __syncthreads();
         for (int k = t; k < j; k += WT) {
             a.hs[k] = hsh[k];

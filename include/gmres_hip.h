@@ -55,7 +55,8 @@ extern "C" {
 #define GK_KID_RES 6     /* resident MGS-R step: whole cascade + norm + scale in one launch */
 #define GK_KID_PREC 7    /* temporal-blocked Chebyshev(k) passes (k_cheb_fused) */
 #define GK_KID_HALO 8    /* halo lines with the slab neighbours (RCCL send/recv, local group or device exchange) */
-#define GK_NKID 9
+#define GK_KID_GRAPH 9   /* one launch-path MGS-R step replayed as a hipGraph (its 2j projections, all-reduces, scale) */
+#define GK_NKID 10
 
 typedef struct gk_ctx gk_ctx;
 typedef struct gk_group gk_group;
@@ -274,7 +275,11 @@ int gk_sync(gk_ctx *ctx);
  *   GK_RES_PAIRS      k_mgs_res<12, 0>: w and the running column in registers;
  *   GK_RES_PAIRS_LDS  k_mgs_res<12, 18>: the same plus w of 18 chunks per
  *                     workgroup in LDS, the rest streamed;
- *   GK_RES_WONLY      k_mgs_wres: w only, in registers + LDS (large slabs).
+ *   GK_RES_WONLY      k_mgs_wres: w only, in registers + LDS (large slabs);
+ *   GK_RES_WCOL       k_mgs_wpc: w in registers and the running Krylov column cached
+ *                     (registers + LDS) -- 8 B per unknown per projection for slabs of
+ *                     up to 64 x 256 double2 per workgroup (one GPU of 4096^2 / 2,
+ *                     4096^2 / 4, 8192^2 / 8).
  * info[GK_RES_INFO_LEN]: variant, workgroups G, R2, L2, prefetch, control
  * wave, w-only, non-temporal column loads, register / LDS chunks per
  * workgroup in use, dynamic LDS bytes, resident double2 of the slab, and
@@ -293,6 +298,7 @@ int gk_sync(gk_ctx *ctx);
 #define GK_RES_PAIRS 2
 #define GK_RES_PAIRS_LDS 3
 #define GK_RES_WONLY 4
+#define GK_RES_WCOL 5
 #define GK_RES_INFO_LEN 14
 int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, long long *info);
 int gk_res_info(gk_ctx *ctx, int hh, long long *info);
@@ -345,6 +351,20 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          and takes the first dot with it (no stencil launch; even N) -- measured
  *                          4 % slower at 4096^2: the prologue's loads cannot be kept in flight beside
  *                          the register-resident w
+ *   GK_TUNE_GRAPH          1 (default): a launch-path MGS-R step (RCCL ranks, or one rank with the
+ *                          resident step off) is captured once per step index j as a hipGraph --
+ *                          its 2j projection launches, 2j + 1 all-reduces (ncclAllReduce captured
+ *                          as graph nodes) and the normalisation -- and replayed in later cycles;
+ *                          0: launched call by call.  A capture that fails switches it off for
+ *                          the context (gk_last_error keeps the reason).
+ *   GK_TUNE_RES_QDEF       k_mgs_res with non-temporal columns (pairs / pairs+lds): 1 = the LDS-held
+ *                          and streamed parts read each pass's dot column V_q with the default
+ *                          policy, so the next pass's AXPY column (the same V_q) is an
+ *                          Infinity-Cache hit (the w-only kernel's policy); 0 = both
+ *                          non-temporal; -1 (default) = the measured choice
+ *   GK_TUNE_RES_PC         column-cache variant (GK_RES_WCOL): -1 (default) where its modelled
+ *                          bytes per projection are strictly below the pairs and w-only
+ *                          variants'; 0 never; 1 wherever the slab fits its registers
  *   GK_TUNE_SPIN_WAIT      1 (default): gk_mgs_step_wait / gk_hh_step_wait spin on the step's
  *                          event; 0: hipEventSynchronize (may sleep in the driver per step) */
 #define GK_TUNE_PROJ_NT 0
@@ -366,6 +386,9 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_CHEB_STEN 16
 #define GK_TUNE_RES_STEN 17
 #define GK_TUNE_SPIN_WAIT 18
+#define GK_TUNE_GRAPH 19
+#define GK_TUNE_RES_QDEF 20
+#define GK_TUNE_RES_PC 21
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */

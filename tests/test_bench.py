@@ -88,9 +88,19 @@ def test_resident_byte_model_follows_the_variant():
     assert sum(r.values()) == n and r["pairs"] == 0 and r["streamed"] / n < 0.02
     per_pass = (bench.res_launch_bytes(p, n, 97) - bench.res_launch_bytes(p, n, 96)) / n
     assert 16.0 < per_pass < 16.4
-    # 4096^2 / 2 and 8192^2 / 8 (k_mgs_res<12, 18> NT): 12 of 32 chunks pairs, 18 in LDS, 2 streamed
+    # 4096^2 / 2 and 8192^2 / 8 (k_mgs_wpc): w in registers, the column cached -> 8 B per unknown
     n, p = _plan(4096, 2)
-    assert p["variant"] == "pairs+lds"
+    assert p["variant"] == "w+column"
+    r = bench.res_regions(p, n)
+    assert r == {"pairs": n, "w_on_chip": 0, "streamed": 0}
+    per_pass = (bench.res_launch_bytes(p, n, 97) - bench.res_launch_bytes(p, n, 96)) / n
+    assert per_pass == pytest.approx(8.0)
+    # the previous kernel of that split (k_mgs_res<12, 18> NT, GK_TUNE_RES_PC 0): 12 of 32 chunks
+    # pairs, 18 in LDS, 2 streamed
+    import gmres_amd as ga
+
+    p = ga.res_plan_query(n, 256, 1, False, 1)
+    p = dict(p, variant="pairs+lds", r2=12, l2=18, r2e=12, l2e=18, nres2=256 * 30 * 512, pf=0, cw=0, wo=0)
     r = bench.res_regions(p, n)
     assert sum(r.values()) == n
     assert r["pairs"] == 2 * 256 * 12 * 512 and r["w_on_chip"] == 2 * 256 * 18 * 512
@@ -121,7 +131,7 @@ def test_roofline_entry_is_a_fraction():
     # a pairs+lds split (4096^2 on 2 GPUs): every byte from DRAM -> bound hbm
     n2, p2 = _plan(4096, 2)
     r2 = bench.roofline_entry(prof, a, n2, 20, 2, p2)
-    assert r2["bound"] == "hbm" and r2["peak"] == bench.HBM_PEAK_GBPS and r2["variant"] == "pairs+lds"
+    assert r2["bound"] == "hbm" and r2["peak"] == bench.HBM_PEAK_GBPS and r2["variant"] == "w+column"
 
 
 def test_cpu_extrapolation_recovers_a_linear_step_cost():

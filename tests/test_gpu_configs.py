@@ -144,7 +144,7 @@ def test_config4_8192_eight_row_block_ranks_on_one_gpu(transport):
         # every Arnoldi step one resident launch per rank, no per-projection launch or
         # all-reduce call: the only all-reduce launches left are the step's first dot
         # (from the stencil's partial slab) and the cycle start's norm
-        assert r["res_G"] == [32] and r["res_launches_min"] >= 95 and r["proj_launches_max"] == 0, r
+        assert r["res_G"] == [32] and r["res_launches_min"] >= 95 and r["proj_launches_max"] <= 1, r  # 1: ||b||
         assert r["comm_launches_max"] <= 95 + 1, r
     else:
         assert r["res_launches_min"] == 0, r

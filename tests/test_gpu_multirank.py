@@ -145,6 +145,47 @@ def test_rccl_one_rank_communicator(monkeypatch, method, prec):
     assert np.array_equal(r.x, ref.x)
 
 
+@pytest.mark.parametrize("rccl", [False, True])
+def test_launch_path_step_graphs(monkeypatch, rccl):
+    """GK_TUNE_GRAPH: the launch-path MGS-R step (2j projection launches, 2j + 1
+    all-reduces -- ncclAllReduce captured as graph nodes on the RCCL path -- and
+    the normalisation) captured once per j and replayed in later cycles gives
+    the call-by-call results bit for bit; the graph replays are what ran (the
+    'graph' profile slot) and the per-step time is recorded for the A/B."""
+    import time
+
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+
+    N, m, cyc = 256, 30, 4
+    out = {}
+    for graph in (0, 1):
+        if rccl:
+            monkeypatch.setenv("GK_FORCE_RCCL", "1")
+        with ga.Context(N, m) as c:
+            if rccl:
+                c.comm_init(1, 0, N, ga.Context.unique_id())
+            c.tune(nat.GK_TUNE_RES, 0)
+            c.tune(nat.GK_TUNE_GRAPH, graph)
+            c.set_rhs_ones()
+            ga.gmres_mgsr(c, 1e-15, max_cycles=1, want_verr=False)  # warm (graphs captured here)
+            c.profile(True)
+            c.profile_reset()
+            c.sync()
+            t0 = time.perf_counter()
+            r = ga.gmres_mgsr(c, 1e-15, max_cycles=cyc, want_hist=True, want_verr=False)
+            c.sync()
+            out[graph] = (r, c.profile_read(), time.perf_counter() - t0)
+    r0, p0, t0 = out[0]
+    r1, p1, t1 = out[1]
+    assert np.array_equal(r0.hist_res, r1.hist_res) and np.array_equal(r0.x, r1.x)
+    assert np.array_equal(r0.final_err, r1.final_err)
+    assert p1["graph"][1] == cyc * m and p1["proj"][1] <= 1, p1  # 1: the solve's ||b||
+    assert p0["graph"][1] == 0 and p0["proj"][1] > 0, p0
+    print(f"launch path {'RCCL' if rccl else 'single'} {N}^2 m={m}: {t0 / cyc * 1e3:.2f} ms/cycle call by call, "
+          f"{t1 / cyc * 1e3:.2f} ms/cycle replayed graphs")
+
+
 @pytest.mark.parametrize("N,nranks", [(66, 3), (20, 4), (16, 5), (130, 2)])
 @pytest.mark.parametrize("degree", [1, 3, 4, 6, 8])
 def test_chebyshev_on_slabs_bitexact(oracle, N, nranks, degree):

@@ -20,10 +20,11 @@ T_RES, T_R2, T_SHARE, T_TMO = 8, 9, 10, 11
 
 
 def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False, wonly=-1, method="mgsr",
-         hh_fuse=1):
+         hh_fuse=1, pc=-1):
     import gmres_amd as ga
 
     with ga.Context(N, m) as c:
+        c.tune(21, pc)  # GK_TUNE_RES_PC
         c.tune(T_RES, res)
         c.tune(15, hh_fuse)  # GK_TUNE_HH_FUSE
         c.tune(13, wonly)  # GK_TUNE_RES_WONLY
@@ -40,6 +41,7 @@ def _run(N, m, prec, res, r2=0, share=1, cycles=4, degree=4, want_prof=False, wo
         else:
             r = ga.gmres_mgsr(c, 1e-15, max_cycles=cycles, want_hist=True)
         prof = c.profile_read() if want_prof else None
+        r.variant = c.res_info(hh=method == "hh")["variant"]
     return r, prof
 
 
@@ -66,10 +68,20 @@ WCASES = [  # w-only variant (one wave per SIMD): few workgroups so the LDS and 
 ]
 
 
-@pytest.mark.parametrize("N,m,prec,r2,share,wonly", [c + (-1,) for c in CASES] + [c + (1,) for c in WCASES])
-def test_resident_matches_launch_path(N, m, prec, r2, share, wonly):
+PCASES = [  # column-cache variant (k_mgs_wpc), forced: cached registers + LDS, streamed rest, odd N
+    (300, 20, "identity", 0, 128),   # 2 workgroups: 88 chunks per thread -> 26 + 38 cached, 24 streamed
+    (181, 16, "cbpr2", 0, 128),      # odd N (tail element), 32 chunks: registers + a few LDS chunks
+    (512, 24, "cheb", 0, 32),        # 8 workgroups x 64 chunks: exactly the 4096^2 / 2 share
+]
+
+
+@pytest.mark.parametrize("N,m,prec,r2,share,wonly,pc", [c + (-1, -1) for c in CASES] + [c + (1, 0) for c in WCASES]
+                         + [c + (-1, 1) for c in PCASES])
+def test_resident_matches_launch_path(N, m, prec, r2, share, wonly, pc):
     ref, _ = _run(N, m, prec, res=0)
-    got, prof = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True, wonly=wonly)
+    got, prof = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True, wonly=wonly, pc=pc)
+    if pc == 1:
+        assert got.variant == "w+column", got.variant
     # the resident kernel ran every step (k_proj only in the off-cycle diagnostics)
     assert prof["res"][1] > 0 and prof["proj"][1] < prof["res"][1] // 4, prof
     assert got.n_cycles == ref.n_cycles
@@ -126,12 +138,18 @@ HCASES = [
     (300, 20, "identity", 12, 64, 1),   # w-only: registers + LDS + streamed
     (181, 16, "cbpr2", 12, 128, 1),     # w-only, odd N
 ]
+HPCASES = [  # the column-cache variant's reflection chains (forced)
+    (300, 20, "identity", 0, 128, 0),
+    (181, 16, "cbpr2", 0, 64, 0),
+]
 
 
-@pytest.mark.parametrize("N,m,prec,r2,share,wonly", HCASES)
-def test_resident_householder_matches_launch_path(N, m, prec, r2, share, wonly):
+@pytest.mark.parametrize("N,m,prec,r2,share,wonly,pc", [c + (-1,) for c in HCASES] + [c + (1,) for c in HPCASES])
+def test_resident_householder_matches_launch_path(N, m, prec, r2, share, wonly, pc):
     ref, _ = _run(N, m, prec, res=0, method="hh")
-    got, prof = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True, wonly=wonly, method="hh")
+    got, prof = _run(N, m, prec, res=1, r2=r2, share=share, want_prof=True, wonly=wonly, method="hh", pc=pc)
+    if pc == 1:
+        assert got.variant == "w+column", got.variant
     assert prof["res"][1] > 0 and prof["proj"][1] < prof["res"][1] // 4, prof  # k_proj: diagnostics only
     assert got.n_cycles == ref.n_cycles
     h, r = got.hist_res, ref.hist_res

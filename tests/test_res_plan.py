@@ -23,16 +23,18 @@ def _plan(N, R, share=1, hh=False, nt=-1):
 @pytest.mark.parametrize("hh", [False, True])
 @pytest.mark.parametrize("N,R,variant,r2e,l2e,nt", [
     (4096, 1, "w-only", None, 38, 1),      # the bench line (config 1), config 3 and 5
-    (4096, 2, "pairs+lds", 12, 18, 1),     # 8.4 M unknowns per GPU
-    (4096, 4, "pairs+lds", 12, 4, 0),      # 4.2 M
-    (4096, 8, "pairs", 8, 0, 0),           # 2.1 M
-    (8192, 8, "pairs+lds", 12, 18, 1),     # config 4: 8.4 M per GPU
+    (4096, 2, "w+column", 64, 0, 1),       # 8.4 M unknowns per GPU: w in registers, its column cached
+    (4096, 4, "w+column", 32, 0, 1),       # 4.2 M
+    (4096, 8, "pairs", 8, 0, 0),           # 2.1 M (w+column ties at 8 B/unknown: the older kernel kept)
+    (8192, 8, "w+column", 64, 0, 1),       # config 4: 8.4 M per GPU
     (1024, 1, "prefetch", 5, 0, 0),        # config 2
 ])
 def test_production_splits(N, R, variant, r2e, l2e, nt, hh):
     p = _plan(N, R, hh=hh)
     assert p["variant"] == variant and p["G"] == 256
     assert p["l2e"] == l2e and p["nt"] == nt
+    if variant == "w+column":  # 26 register + 38 LDS chunks of the column: all of a 64-chunk share cached
+        assert (p["r2"], p["l2"], p["lds"]) == (26, 38, 38 * 256 * 16)
     if r2e is not None:
         assert p["r2e"] == r2e
     else:  # w-only: 88 (MGS-R) / 90 (reflection chains) register chunks of 256 double2
@@ -50,7 +52,7 @@ def test_ranks_on_one_gpu_carry_the_production_load(N, prod, R):
     assert t["G"] == 256 // R and p["G"] == 256 and t["nt"] == p["nt"]
     for k in ("variant", "r2e", "l2e"):
         assert t[k] == p[k], (k, t, p)
-    dt = 256 if p["variant"] == "w-only" else 512
+    dt = 256 if p["variant"] in ("w-only", "w+column") else 512
     # resident double2 per workgroup agree within one chunk (ragged last chunk)
     assert abs(t["nres2"] / t["G"] - p["nres2"] / p["G"]) <= dt
 
