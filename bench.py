@@ -463,22 +463,40 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: d
         roof["ceiling"] = "hbm: every compulsory byte is a DRAM byte (non-temporal column loads / register reuse)"
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf) and on_res and args.method == "mgsr":
-        key = pmc_key(variant, nloc, m, args.prec, args.method)
-        pm = json.load(open(tf)).get(key)
+        key, scale = pmc_lookup(json.load(open(tf)), variant, nloc, m, args.prec, args.method)
+        pm = json.load(open(tf)).get(key) if key else None
         if pm and bool(pm.get("sten", False)) != sten:  # measured on the other step flow: not this kernel's bytes
             pm = None
         if pm and "per_step" in pm:
-            per_step = {int(k): v for k, v in pm["per_step"].items()}
+            per_step = {int(k): v * scale for k, v in pm["per_step"].items()}
             if all(j in per_step for j in set(steps_js)):
                 tb = sum(per_step[j] for j in steps_js) / len(steps_js)
                 roof["traffic"] = round(tb)
-                roof["traffic_source"] = pm["source"]
+                roof["traffic_source"] = pm["source"] + (f" (scaled x{scale:.5f} from the {pm.get('nloc')}-unknown "
+                                                         f"slab it was measured on)" if scale != 1.0 else "")
                 roof["traffic_key"] = key
                 roof["physical"] = {"fabric_GBps": round(tb * launches / secs / 1e9, 1),
                                     "traffic_over_alg": round(tb * launches / fused, 3),
                                     "note": "FETCH_SIZE (x2, gfx950) + WRITE_SIZE at the same steps j: L2<->fabric "
                                             "bytes, Infinity-Cache hits included"}
     return roof
+
+
+def pmc_lookup(db: dict, variant: str, nloc: int, m: int, prec: str, method: str) -> tuple[str | None, float]:
+    """The PMC entry of this kernel: the exact slab, else the same variant on a
+    slab within 2 % of this one (4096^2 / 2 and 8192^2 / 8 have 8,388,608
+    unknowns per GPU, the single-GPU stand-in 2896^2 has 8,386,816), its bytes
+    scaled by the unknown count."""
+    key = pmc_key(variant, nloc, m, prec, method)
+    if key in db:
+        return key, 1.0
+    best = None
+    for k, v in db.items():
+        if (k.startswith(f"res_{variant}_") and k.endswith(f"_{m}_{prec}_{method}") and v.get("nloc")
+                and abs(v["nloc"] - nloc) <= 0.02 * nloc):
+            if best is None or abs(v["nloc"] - nloc) < abs(db[best]["nloc"] - nloc):
+                best = k
+    return (best, nloc / db[best]["nloc"]) if best else (None, 1.0)
 
 
 def pmc_key(variant: str, nloc: int, m: int, prec: str, method: str) -> str:
@@ -699,7 +717,8 @@ def main() -> None:
     line0, nlines = parts[rank]
     ctx = ga.Context(N, m, device=local, line0=line0, nlines=nlines)
     if same_dev and world > 1:
-        ctx.tune(10, world)  # GK_TUNE_RES_SHARE
+        ctx.tune(10, world)  # GK_TUNE_RES_SHARE: 256 / N workgroups per rank
+        ctx.tune(8, 1)  # GK_TUNE_RES: resident steps on (auto mode assumes one context per device)
     ml = max(p[1] for p in parts)
     collective = None
     rccl_failed = None  # RCCL init failed on some rank; the device exchange carries every collective

@@ -81,15 +81,15 @@ def _scratch_kernels(remarks: str, name: str) -> list[str]:
 
 def _compile_link(so: str, defines: list[str]) -> None:
     """Compile the HIP translation units in parallel into objects beside `so`,
-    then link them into the shared library.  The Chebyshev pass must not spill
-    registers to scratch (gk_cheb.hip refuses such kernels at run time): the
-    build fails here already, naming them."""
+    then link them into the shared library.  The Chebyshev pass and the resident
+    step kernels must not spill registers to scratch (gk_cheb.hip refuses such a
+    pass at run time; a spilled resident kernel holds w in scratch memory): the
+    build fails here, naming them."""
     objs, procs = [], []
     for src, unit_defs, oname in HIP_UNITS:
         obj = os.path.join(os.path.dirname(so), oname)
-        cmd = [hipcc(), *HIP_FLAGS, *[f"-D{x}" for x in defines + unit_defs], "-c", src, "-o", obj]
-        if unit_defs:
-            cmd.append("-Rpass-analysis=kernel-resource-usage")
+        cmd = [hipcc(), *HIP_FLAGS, *[f"-D{x}" for x in defines + unit_defs], "-c", src, "-o", obj,
+               "-Rpass-analysis=kernel-resource-usage"]
         print("+", " ".join(cmd), flush=True)
         procs.append(subprocess.Popen(cmd, stderr=subprocess.PIPE, text=True))
         objs.append(obj)
@@ -97,11 +97,12 @@ def _compile_link(so: str, defines: list[str]) -> None:
     for p in procs:
         err = p.communicate()[1]
         sys.stderr.write("".join(l + "\n" for l in err.splitlines() if "warning:" in l or "error" in l))
-        bad += _scratch_kernels(err, "k_cheb_fused")
+        for name in ("k_cheb_fused", "k_mgs_wpc", "k_mgs_wres", "k_mgs_res"):
+            bad += _scratch_kernels(err, name)
     if any(p.returncode for p in procs):
         raise subprocess.CalledProcessError(max(p.returncode for p in procs), "hipcc")
     if bad:
-        raise RuntimeError(f"Chebyshev pass kernels spill to scratch: {bad}")
+        raise RuntimeError(f"kernels built with a register spill to scratch (refused): {bad}")
     _run([hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", *objs, "-o", so, "-lrccl"])
     for o in objs:
         os.remove(o)

@@ -669,8 +669,20 @@ struct ResPlan {
 // Column-cache variant (k_mgs_wpc): w of up to RES_PC_RW chunks per thread in
 // registers, the running column of RES_PC_RX of them in registers and of
 // RES_PC_LX in LDS (26 + 38 = all 64: the slab of one GPU of 4096^2 / 2 and of
-// 8192^2 / 8).
+// 8192^2 / 8).  A pass streams the one column it reads in batches of WB chunks,
+// software-pipelined (batch b + 1 in flight while b is consumed).  Without the
+// pipeline the pass was latency-bound -- 8.4 us for 33.5 MB at 2048^2 with
+// 8-chunk batches, and 16-chunk batches were slower still (9.4 us,
+// profiles/r04/ab_wpc_r04c.jsonl); 8 for the MGS step, 6 for the reflection
+// chains (8 spills there).
+#ifndef GK_RES_PC_WB
+#define GK_RES_PC_WB 8
+#endif
+#ifndef GK_RES_PC_WB_HH
+#define GK_RES_PC_WB_HH 6
+#endif
 constexpr int RES_PC_RW = 64, RES_PC_RX = 26, RES_PC_LX = 38;
+constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH;
 
 // Modelled bytes per projection of a slab of n2 double2 on G workgroups (the
 // unit of pairs_bytes / wonly_bytes: 8 per double2 whose w and running column are
@@ -867,14 +879,16 @@ int launch_wres(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 
 template <int MODE>
 int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    constexpr int WBT = MODE == gk::RES_MGS ? RES_PC_WB : RES_PC_WB_HH;
     static std::atomic<int> attr[ATTR_DEVS];
     if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
     if (attr[c->dev].load() < p.lds) {
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
+        HIPCHK(hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
         attr[c->dev] = p.lds;
     }
-    gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE><<<p.G, gk::WT, p.lds, c->st>>>(a);
+    gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT><<<p.G, gk::WT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
 }

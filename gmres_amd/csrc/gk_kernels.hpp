@@ -2060,15 +2060,16 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
             if (c0 + RX + k < cend) lx[k * WT + t] = ldv<true>(C2 + (c0 + RX + k) * WT + t);
     }
     // One pass: w -= ch V_i (the cached column; V_i from HBM past the cache), then
-    // the reduction `kind`; with a dot, V_q replaces the cached column.
+    // the reduction `kind`; with a dot, V_q replaces the cached column.  Software-
+    // pipelined: the loads of batch b + 1 are issued before batch b is consumed,
+    // two batch buffers in registers, so a wave always has a batch in flight (one
+    // wave per SIMD: nothing else hides the latency).
     auto pass = [&](double ch, int i, int q, int kind) -> double {
         const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
         const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
         const bool dot = kind == RK_DOT;
         double acc = 0.0;
-#pragma unroll
-        for (int k0 = 0; k0 < RW; k0 += WBT) {
-            double2 av[WBT], bv[WBT];
+        auto issue = [&](int k0, double2 (&av)[WBT], double2 (&bv)[WBT]) {
 #pragma unroll
             for (int u = 0; u < WBT; ++u) {
                 const int k = k0 + u;
@@ -2078,6 +2079,8 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
                     if (k >= RX + LX) av[u] = ldv<true>(A2 + c * WT + t);  // not cached
                 }
             }
+        };
+        auto consume = [&](int k0, const double2 (&av)[WBT], const double2 (&bv)[WBT]) {
 #pragma unroll
             for (int u = 0; u < WBT; ++u) {
                 const int k = k0 + u;
@@ -2102,6 +2105,17 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
                         sq_acc(acc, wr[k], (c0 + k) * WT + t, tail0, mode == RES_HH_UP && c0 + k == 0);
                     }
                 }
+            }
+        };
+        double2 a0[WBT], b0[WBT], a1[WBT], b1[WBT];
+        issue(0, a0, b0);
+#pragma unroll
+        for (int k0 = 0; k0 < RW; k0 += 2 * WBT) {
+            if (k0 + WBT < RW) issue(k0 + WBT, a1, b1);
+            consume(k0, a0, b0);
+            if (k0 + WBT < RW) {
+                if (k0 + 2 * WBT < RW) issue(k0 + 2 * WBT, a0, b0);
+                consume(k0 + WBT, a1, b1);
             }
         }
         for (i64 e0 = sbase; e0 < n2; e0 += 2 * sstride) {  // streamed part: 32 B/unknown

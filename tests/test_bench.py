@@ -236,3 +236,17 @@ def test_control_plane_world_size(world, tmp_path):
         assert o["all"] == [10 * k for k in range(world)] and o["b"] == "root"
         assert o["min"] == 1 and o["max"] == world - 0.5 and o["sum"] == world * (world - 1) // 2
     assert not os.path.exists(os.path.join(str(tmp_path), "gk_ctl_t"))  # rank 0 removed the rendezvous file
+
+
+def test_pmc_lookup_by_variant_and_slab():
+    """profiles/pmc_traffic.json is keyed by the resident variant and the slab it
+    ran on; a split whose per-GPU slab is within 2 % of a measured one (4096^2 / 2
+    vs the 2896^2 stand-in) reuses it scaled by the unknown count."""
+    import json
+
+    db = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    k, s = bench.pmc_lookup(db, "w-only", 4096 * 4096, 95, "identity", "mgsr")
+    assert k == "res_w-only_16777216_95_identity_mgsr" and s == 1.0
+    k, s = bench.pmc_lookup(db, "w+column", 4096 * 4096 // 2, 95, "identity", "mgsr")
+    assert k == "res_w+column_8386816_95_identity_mgsr" and s == pytest.approx(8388608 / 8386816)
+    assert bench.pmc_lookup(db, "w+column", 4096 * 4096, 95, "identity", "mgsr") == (None, 1.0)

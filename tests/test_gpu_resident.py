@@ -69,7 +69,7 @@ WCASES = [  # w-only variant (one wave per SIMD): few workgroups so the LDS and 
 
 
 PCASES = [  # column-cache variant (k_mgs_wpc), forced: cached registers + LDS, streamed rest, odd N
-    (300, 20, "identity", 0, 128),   # 2 workgroups: 88 chunks per thread -> 26 + 38 cached, 24 streamed
+    (300, 20, "identity", 0, 64),    # 4 workgroups x 44 chunks (26 in registers, 18 in LDS), a streamed tail
     (181, 16, "cbpr2", 0, 128),      # odd N (tail element), 32 chunks: registers + a few LDS chunks
     (512, 24, "cheb", 0, 32),        # 8 workgroups x 64 chunks: exactly the 4096^2 / 2 share
 ]
@@ -139,7 +139,7 @@ HCASES = [
     (181, 16, "cbpr2", 12, 128, 1),     # w-only, odd N
 ]
 HPCASES = [  # the column-cache variant's reflection chains (forced)
-    (300, 20, "identity", 0, 128, 0),
+    (300, 20, "identity", 0, 64, 0),
     (181, 16, "cbpr2", 0, 64, 0),
 ]
 

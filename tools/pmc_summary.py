@@ -18,6 +18,8 @@ import json
 import os
 import statistics
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def per_launch(path, kernel):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
@@ -46,18 +48,30 @@ def res_fit(a):
     js = np.arange(1, a.probe_m + 1)
     b, c = np.polyfit(2 * js, y, 1)
     n = a.grid * a.grid // a.gpus
-    entry = {"kernel": a.kernel, "launches_sampled": int(a.probe_m), "bytes_fixed": float(c),
+    # the byte model of the variant that ran (bench.res_launch_bytes, the roofline's)
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+    import gmres_amd as ga
+
+    nl = max(k for _, k in ga.slab_partition(a.grid, a.gpus))
+    plan = ga.res_plan_query(a.grid * nl, 256, 1, a.method == "hh", -1)
+    if a.variant and plan["variant"] != a.variant:
+        raise SystemExit(f"the plan query selects {plan['variant']}, not {a.variant}")
+    model = {int(j): bench.res_launch_bytes(plan, n, 2 * int(j), mgs=True, sten=a.sten) for j in js}
+    entry = {"kernel": a.kernel, "variant": plan["variant"], "nloc": n, "launches_sampled": int(a.probe_m),
+             "bytes_fixed": float(c),
              "bytes_per_projection": float(b), "bytes_per_unknown_per_projection": float(b) / n,
              "fit_residual_max_rel": float(np.max(np.abs(y - (b * 2 * js + c)) / y)),
              "per_step": {str(int(j)): float(v) for j, v in zip(js, y)},
-             "per_step_fused_model_ratio": {str(int(j)): float(v / ((32 * j + 16 + (8 if a.sten else 0)) * n))
-                                            for j, v in zip(js, y) if j % 16 == 0},
+             "per_step_model_ratio": {str(int(j)): float(v / model[int(j)]) for j, v in zip(js, y) if j % 16 == 0},
              "sten": bool(a.sten),
              "source": f"{os.path.relpath(a.fetch)} + {os.path.relpath(a.write)} (every launch j = 1..{a.probe_m} "
                        "of one full cycle, FETCH_SIZE x2 gfx950 correction; L2<->fabric bytes incl. "
                        "Infinity-Cache hits)"}
     db = json.load(open(a.out)) if os.path.exists(a.out) else {}
-    db[f"{a.grid}_{a.m}_{a.prec}_{a.method}_{a.gpus}_res"] = entry
+    db[bench.pmc_key(plan["variant"], n, a.m, a.prec, a.method)] = entry
     json.dump(db, open(a.out, "w"), indent=1)
     print(json.dumps({k: v for k, v in entry.items() if k != "per_step"}, indent=1))
 
@@ -76,6 +90,7 @@ def main():
                     help="resident-step kernel (one launch per Arnoldi step j = 1..probe-m in launch order): "
                          "fit bytes per launch = fixed + per_projection * 2j")
     ap.add_argument("--probe-m", type=int, default=95, help="resident launches of the traced cycle (= m)")
+    ap.add_argument("--variant", default=None, help="the resident variant expected to have run (checked)")
     ap.add_argument("--sten", action="store_true",
                     help="the step launches formed w = A V(:,j) themselves (gk_res_info sten; model +8n)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),

@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""A falsifiable prediction of the strong-scaling curve (4096^2 on 1/2/4/8 GPUs)
+and of config 4 (8192^2 on 8 GPUs), regenerated from committed single-GPU
+measurements.
+
+Model.  An N-rank run gives every GPU a slab of n/N unknowns; its Arnoldi steps
+run the resident kernel that slab selects (tests/test_res_plan.py), on all 256
+CUs, exactly as a single-GPU run of a grid with the same unknown count does
+(1448^2 ~ 4096^2/8, 2048^2 ~ 4096^2/4, 2896^2 ~ 4096^2/2 and 8192^2/8).  So the
+per-GPU cycle time is that single-GPU cycle (bench.py --grid G, ms_per_step)
+plus what only N ranks pay:
+  * per Arnoldi step, two collective launches on the step's critical path: the
+    halo lines before the stencil (k_xhalo) and the all-reduce of the stencil's
+    fused first dot (k_xchg) -- priced at gk_comm_latency's per-call times;
+  * per projection, the hop of the rank totals inside the resident launch
+    (workgroup 0 of every rank stores its total into every peer's region over
+    xGMI, every workgroup polls its own region): delta_hop.
+  t_cycle(N) = t_cycle_1GPU(n/N) + m (t_halo + t_allreduce) + m (m + 1) delta_hop
+  it/s(N)    = m / t_cycle(N),  value of the N-GPU bench line (max over ranks).
+The collective per-call times come from a same-device rehearsal (two processes
+on one GPU through IPC: no xGMI hop, so a LOWER bound); delta_hop is bracketed
+by [lo, hi] (default 1..4 us: one uncached store crossing xGMI and a poll).
+Each SCALE line carries diagnostics.resident_split_per_unit_us (the measured
+wait per projection) and collective_latency_us, against which the predicted
+terms can be read directly.
+
+  python tools/predict_scaling.py [--hop-lo 1.0] [--hop-hi 4.0] [--out profiles/r04/scaling_prediction_r04.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+M = 95
+
+# per-GPU load of each point -> the single-GPU bench line measured at that load
+POINTS = [
+    # (label, world, global grid, equal-load single-GPU grid, bench JSON under profiles/)
+    ("4096^2 on 1 GPU", 1, 4096, 4096, "r04/bench_default_r04b.json"),
+    ("4096^2 on 2 GPUs", 2, 4096, 2896, "r04/bench_2896_r04b.json"),
+    ("4096^2 on 4 GPUs", 4, 4096, 2048, "r04/bench_2048_r04b.json"),
+    ("4096^2 on 8 GPUs", 8, 4096, 1448, "r04/bench_1448_r04b.json"),
+    ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r04/bench_2896_r04b.json"),
+]
+COMM = "r04/rehearsal_comm_latency_r04b.json"  # {"allreduce_us": .., "halo_us": ..} (same-device, 2 processes)
+
+
+def load(rel: str) -> dict | None:
+    p = os.path.join(ROOT, "profiles", rel)
+    if not os.path.exists(p):
+        return None
+    txt = open(p).read().strip().splitlines()
+    return json.loads([x for x in txt if x.startswith("{")][-1])
+
+
+def predict(hop_lo: float, hop_hi: float) -> dict:
+    comm = load(COMM) or {}
+    t_ar, t_halo = float(comm.get("allreduce_us", 10.0)), float(comm.get("halo_us", 10.0))
+    rows = []
+    for label, world, grid, g1, rel in POINTS:
+        b = load(rel)
+        if b is None:
+            rows.append({"point": label, "missing": rel})
+            continue
+        t1 = float(b["ms_per_step"]) * 1e-3  # one cycle of the equal-load single-GPU run
+        split = ((b.get("diagnostics") or {}).get("resident_split_per_unit_us") or {}).get("mgs_step") or {}
+        extra_fixed = 0.0 if world == 1 else M * (t_ar + t_halo) * 1e-6
+        nproj = M * (M + 1)
+        lo = t1 + extra_fixed + (0.0 if world == 1 else nproj * hop_lo * 1e-6)
+        hi = t1 + extra_fixed + (0.0 if world == 1 else nproj * hop_hi * 1e-6)
+        rows.append({
+            "point": label, "world": world, "grid": grid, "per_gpu_unknowns": grid * grid // world,
+            "equal_load_grid": g1, "variant": (b.get("config") or {}).get("resident_variant"),
+            "t_cycle_1gpu_ms": round(t1 * 1e3, 2),
+            "per_projection_1gpu_us": (b.get("roofline") or {}).get("per_projection_us"),
+            "pass_us": split.get("pass_us"), "wait_us": split.get("wait_us"),
+            "collective_ms_per_cycle": round(extra_fixed * 1e3, 2),
+            "hop_ms_per_cycle": [round(nproj * hop_lo * 1e-3, 2), round(nproj * hop_hi * 1e-3, 2)] if world > 1 else 0,
+            "predicted_ms_per_cycle": [round(lo * 1e3, 1), round(hi * 1e3, 1)],
+            "predicted_it_s": [round(M / hi, 1), round(M / lo, 1)],
+            "predicted_wait_per_projection_us": ([round((split.get("wait_us") or 0) + hop_lo, 2),
+                                                  round((split.get("wait_us") or 0) + hop_hi, 2)] if world > 1 else
+                                                 split.get("wait_us")),
+            "source": f"profiles/{rel}",
+        })
+    base = next((r for r in rows if r.get("world") == 1), None)
+    for r in rows:
+        if base and "predicted_it_s" in r and r["grid"] == 4096:
+            r["predicted_speedup"] = [round(v / base["predicted_it_s"][1], 2) for v in r["predicted_it_s"]]
+    return {"model": "t_cycle(N) = t_cycle_1GPU(n/N) + m (t_halo + t_allreduce) + m (m+1) delta_hop",
+            "m": M, "collective_per_call_us": {"allreduce": t_ar, "halo": t_halo, "source": f"profiles/{COMM}"
+                                                if comm else "default 10 us (no rehearsal file)"},
+            "delta_hop_us": [hop_lo, hop_hi], "points": rows}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--hop-lo", type=float, default=1.0)
+    ap.add_argument("--hop-hi", type=float, default=4.0)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04", "scaling_prediction_r04.json"))
+    a = ap.parse_args()
+    out = predict(a.hop_lo, a.hop_hi)
+    json.dump(out, open(a.out, "w"), indent=1)
+    print("| point | variant | 1-GPU cycle at the per-GPU load (ms) | predicted ms / cycle | predicted it/s |"
+          " predicted wait / projection (us) |")
+    print("|---|---|---|---|---|---|")
+    for r in out["points"]:
+        if "missing" in r:
+            print(f"| {r['point']} | missing {r['missing']} | | | | |")
+            continue
+        print(f"| {r['point']} | {r['variant']} | {r['t_cycle_1gpu_ms']} | {r['predicted_ms_per_cycle'][0]}-"
+              f"{r['predicted_ms_per_cycle'][1]} | {r['predicted_it_s'][0]}-{r['predicted_it_s'][1]} | "
+              f"{r['predicted_wait_per_projection_us']} |")
+
+
+if __name__ == "__main__":
+    main()
