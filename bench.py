@@ -708,7 +708,14 @@ def main() -> None:
         sys.exit(2)
     from gmres_amd.ctl import Ctl
 
+    t_start = time.perf_counter()
+
+    def log(stage: str) -> None:  # progress on stderr: a long multi-rank run is never silent
+        print(f"[bench rank {rank}/{world} +{time.perf_counter() - t_start:.1f}s] {stage}", file=sys.stderr,
+              flush=True)
+
     ctl = Ctl(rank, world)  # out-of-band control plane (TCP on loopback); a no-op for one rank
+    log("control plane up")
 
     import gmres_amd as ga
 
@@ -745,6 +752,7 @@ def main() -> None:
     if world > 1 and args.collective in ("auto", "xgmi"):
         collective = setup_xgmi(ctx, ctl, rank,
                                 required=args.collective == "xgmi" or rccl_failed is not None) or "rccl"
+    log(f"collective: {collective or 'none'}")
     for kv in args.tune:
         k, v = kv.split("=")
         ctx.tune(int(k), int(v))
@@ -776,6 +784,7 @@ def main() -> None:
 
     fallback = None
     ok, why = guarded_warmup()
+    log(f"warmup {'done' if ok else 'FAILED'}")
     if not ok:
         # Fallback, decided by all ranks together and REPORTED in the JSON line:
         # the launch-per-projection path, and RCCL instead of the device exchange
@@ -806,10 +815,12 @@ def main() -> None:
     resid = ctx.true_residual()  # outside the timed region; same value at any N
     comm = ctx.comm_info()
     elapsed = ctl.allreduce(t1 - t0, "max")
+    log(f"timed {args.steps} cycle(s): {elapsed * 1e3:.1f} ms")
     cycles = res.n_cycles
     iters = (cycles - 1) * m + res.n_out if cycles > 0 else 0
     plan = ctx.res_info(hh=args.method == "hh")  # the resident variant the timed launches ran
     diag = None if args.no_diag else diagnostics(ctx, args, run, ctl, world)
+    log("diagnostics done")
     if diag is not None:
         diag["pcie_inclusive"] = pcie_inclusive(ctx, args, run, ctl, line0, nlines)
 
@@ -821,6 +832,7 @@ def main() -> None:
     legs = None
     if rank == 0 and world == 1 and not args.no_configs and (N, m, args.prec, args.method) == (4096, 95, "identity",
                                                                                                  "mgsr"):
+        log("BASELINE config legs")
         legs = config_legs(ga, args.prof_every)
     if rank == 0:
         n = N * N
@@ -830,6 +842,7 @@ def main() -> None:
         b_written = cycle_bytes(n, m, args.prec, args.degree, args.method, "as_written", sten) * cycles
         cpu = None
         if not args.no_cpu and world == 1:
+            log("CPU baseline (the reference on this host)")
             cpu = cpu_baseline(N, m, args.prec, args.degree, args.method, args.cpu_cap, args.cpu_steps)
         check = {"true_rel_residual_after_timed_cycles": resid}
         if "res" in warm and len(warm["res"].hist_res) > 0:

@@ -323,8 +323,36 @@ int res_check(gk_ctx *c) {
     return GK_OK;
 }
 
+// Host-side watchdog of every wait on this context's stream: the device waits
+// all carry deadlines, but a kernel that is never SCHEDULED (its queue not mapped:
+// more processes / streams on a device than its hardware queues) would keep the
+// host waiting forever.  Past twice the longest device deadline plus a minute,
+// the wait fails with GK_ERR_COMM instead.
+long long watchdog_ms(const gk_ctx *c) { return 2LL * std::max(c->res_timeout_ms, c->xs_timeout_ms) + 60000; }
+
+int spin_until(gk_ctx *c, hipError_t (*query)(void *), void *obj, const char *what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 1;; ++it) {
+        const hipError_t r = query(obj);
+        if (r == hipSuccess) return GK_OK;
+        if (r != hipErrorNotReady) return set_err(GK_ERR_HIP, "%s: %s", what, hipGetErrorString(r));
+        if ((it & 1023u) == 0) {
+            const long long ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                                     std::chrono::steady_clock::now() - t0).count();
+            if (ms > watchdog_ms(c))
+                return set_err(GK_ERR_COMM,
+                               "%s: not complete after %lld ms (rank %d of %d): a kernel of this context was never "
+                               "scheduled -- more streams on the device than hardware queues?",
+                               what, ms, c->rank, c->nranks);
+        }
+    }
+}
+
+hipError_t query_stream(void *s) { return hipStreamQuery(static_cast<hipStream_t>(s)); }
+hipError_t query_event(void *e) { return hipEventQuery(static_cast<hipEvent_t>(e)); }
+
 int sync_st(gk_ctx *c) {
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(spin_until(c, query_stream, c->st, "stream synchronize"));
     CHK(res_check(c));
     return xs_check(c);
 }
@@ -669,20 +697,22 @@ struct ResPlan {
 // Column-cache variant (k_mgs_wpc): w of up to RES_PC_RW chunks per thread in
 // registers, the running column of RES_PC_RX of them in registers and of
 // RES_PC_LX in LDS (26 + 38 = all 64: the slab of one GPU of 4096^2 / 2 and of
-// 8192^2 / 8).  A pass streams the one column it reads in batches of WB chunks,
-// software-pipelined (batch b + 1 in flight while b is consumed).  Without the
-// pipeline the pass was latency-bound -- 8.4 us for 33.5 MB at 2048^2 with
-// 8-chunk batches, and 16-chunk batches were slower still (9.4 us,
-// profiles/r04/ab_wpc_r04c.jsonl); 8 for the MGS step, 6 for the reflection
-// chains (8 spills there).
+// 8192^2 / 8).  A pass streams the one column it reads in batches of WB chunks
+// (8 measured best: 4, 16 and a software-pipelined 8 were slower,
+// profiles/r04/ab_wpc_r04c.jsonl / ab_wpc_r04d.jsonl); the reflection chains
+// keep 6 (8 spills there).  During each all-gather the first PC_TOUCH chunks of
+// the next pass's dot column are touched into L2 (paced, as the w-only step).
 #ifndef GK_RES_PC_WB
 #define GK_RES_PC_WB 8
 #endif
 #ifndef GK_RES_PC_WB_HH
 #define GK_RES_PC_WB_HH 6
 #endif
+#ifndef GK_RES_PC_TOUCH
+#define GK_RES_PC_TOUCH 28
+#endif
 constexpr int RES_PC_RW = 64, RES_PC_RX = 26, RES_PC_LX = 38;
-constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH;
+constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH, RES_PC_TOUCH = GK_RES_PC_TOUCH;
 
 // Modelled bytes per projection of a slab of n2 double2 on G workgroups (the
 // unit of pairs_bytes / wonly_bytes: 8 per double2 whose w and running column are
@@ -884,11 +914,11 @@ int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
     if (attr[c->dev].load() < p.lds) {
         HIPCHK(hipFuncSetAttribute(
-            reinterpret_cast<const void *>(&gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT>),
+            reinterpret_cast<const void *>(&gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT, RES_PC_TOUCH>),
             hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
         attr[c->dev] = p.lds;
     }
-    gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT><<<p.G, gk::WT, p.lds, c->st>>>(a);
+    gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT, RES_PC_TOUCH><<<p.G, gk::WT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
 }
@@ -2065,11 +2095,7 @@ int wait_step_event(gk_ctx *c, hipEvent_t e) {
         HIPCHK(hipEventSynchronize(e));
         return GK_OK;
     }
-    for (;;) {
-        const hipError_t r = hipEventQuery(e);
-        if (r == hipSuccess) return GK_OK;
-        if (r != hipErrorNotReady) return set_err(GK_ERR_HIP, "event query: %s", hipGetErrorString(r));
-    }
+    return spin_until(c, query_event, e, "Arnoldi step wait");
 }
 
 int gk_mgs_step_wait(gk_ctx *c, int j, double *hcol) {

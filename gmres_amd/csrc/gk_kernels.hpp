@@ -2028,10 +2028,11 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 // k_mgs_res / k_mgs_wres; only the dot summation order within a thread
 // differs.  Columns non-temporal (nothing is re-read through the caches).
 // --------------------------------------------------------------------------
-template <int RW, int RX, int LX, int MODE, int WBT = 8>
+template <int RW, int RX, int LX, int MODE, int WBT = 8, int TCHP = 0>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
     static_assert(RX <= RW && RX + LX <= RW, "the column cache covers register chunks of w only");
     extern __shared__ double2 lx[];  // [LX][WT]: cached column of chunks RX .. RX + LX - 1
+    __shared__ int xdone;            // the exchange in progress has completed (stops the touches)
     __shared__ double sm[WT / 64];
     __shared__ double bc[1];
     __shared__ int okf;
@@ -2060,16 +2061,18 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
             if (c0 + RX + k < cend) lx[k * WT + t] = ldv<true>(C2 + (c0 + RX + k) * WT + t);
     }
     // One pass: w -= ch V_i (the cached column; V_i from HBM past the cache), then
-    // the reduction `kind`; with a dot, V_q replaces the cached column.  Software-
-    // pipelined: the loads of batch b + 1 are issued before batch b is consumed,
-    // two batch buffers in registers, so a wave always has a batch in flight (one
-    // wave per SIMD: nothing else hides the latency).
+    // the reduction `kind`; with a dot, V_q replaces the cached column.  Batches of
+    // WBT chunks (A/B, profiles/r04/ab_wpc_r04d.jsonl: software-pipelining the
+    // batches -- batch b + 1 issued before b is consumed -- was slower, 17.5 ->
+    // 18.3 us per projection at 2896^2, and so were 4- and 16-chunk batches).
     auto pass = [&](double ch, int i, int q, int kind) -> double {
         const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
         const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
         const bool dot = kind == RK_DOT;
         double acc = 0.0;
-        auto issue = [&](int k0, double2 (&av)[WBT], double2 (&bv)[WBT]) {
+#pragma unroll
+        for (int k0 = 0; k0 < RW; k0 += WBT) {
+            double2 av[WBT], bv[WBT];
 #pragma unroll
             for (int u = 0; u < WBT; ++u) {
                 const int k = k0 + u;
@@ -2079,8 +2082,6 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
                     if (k >= RX + LX) av[u] = ldv<true>(A2 + c * WT + t);  // not cached
                 }
             }
-        };
-        auto consume = [&](int k0, const double2 (&av)[WBT], const double2 (&bv)[WBT]) {
 #pragma unroll
             for (int u = 0; u < WBT; ++u) {
                 const int k = k0 + u;
@@ -2105,17 +2106,6 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
                         sq_acc(acc, wr[k], (c0 + k) * WT + t, tail0, mode == RES_HH_UP && c0 + k == 0);
                     }
                 }
-            }
-        };
-        double2 a0[WBT], b0[WBT], a1[WBT], b1[WBT];
-        issue(0, a0, b0);
-#pragma unroll
-        for (int k0 = 0; k0 < RW; k0 += 2 * WBT) {
-            if (k0 + WBT < RW) issue(k0 + WBT, a1, b1);
-            consume(k0, a0, b0);
-            if (k0 + WBT < RW) {
-                if (k0 + 2 * WBT < RW) issue(k0 + 2 * WBT, a0, b0);
-                consume(k0 + WBT, a1, b1);
             }
         }
         for (i64 e0 = sbase; e0 < n2; e0 += 2 * sstride) {  // streamed part: 32 B/unknown
@@ -2154,20 +2144,42 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
         }
         return acc;
     };
+    // The all-gather; meanwhile waves 1..3 touch the first TCHP chunks of the NEXT
+    // pass's dot column (one dword per 128-B line into a sink register, paced, up
+    // to the moment wave 0 holds the total), so that pass starts on lines already
+    // in L2 instead of paying the stream's ramp-up after every exchange (the pass
+    // time was ~3.3 us + bytes / 5.7 TB/s over 1448^2..2896^2, r04d).
     int xi = 0;
-    auto reduce = [&](double acc, double &h) -> bool {
+    int touch_sink = 0;
+    auto reduce = [&](double acc, double &h, int touch_col) -> bool {
         clk.passed(a.stamps);
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
+        if (t == 0) xdone = 0;
         __syncthreads();
-        if (t < 64) res_exchange<WT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
+        if (t < 64) {
+            res_exchange<WT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
+            if (t == 0) *(volatile int *)&xdone = 1;
+        } else if constexpr (TCHP > 0) {
+            if (touch_col >= 0) {
+                const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + c0 * WT);
+                const i64 nc = cend - c0 < TCHP ? (cend - c0 > 0 ? cend - c0 : 0) : TCHP;
+                for (i64 l = t - 64; l < 32 * nc; l += WT - 64) {
+                    if (*(volatile int *)&xdone) break;  // wave-uniform: one LDS word
+                    asm volatile("global_load_dword %0, %1, off" : "+v"(touch_sink) : "v"(base + l * 128) : "memory");
+                    __builtin_amdgcn_s_sleep(TOUCH_PACE);
+                }
+            }
+        }
         __syncthreads();
+        if constexpr (TCHP > 0) asm volatile("s_waitcnt vmcnt(0)" : : "v"(touch_sink) : "memory");
         ++xi;
         h = bc[0];
         clk.waited(a.stamps);
         return okf != 0;
     };
     auto kind_of = [&](int p) { return p < np - 1 ? RK_DOT : (mode == RES_HH_DOWN ? RK_NONE : RK_NORM); };
+    auto next_dot_col = [&](int p) { return p + 1 < np && kind_of(p + 1) == RK_DOT ? res_col(mode, j, p + 2) : -1; };
     double h;
     bool ok = true;
     if (mode == RES_HH_DOWN) {
@@ -2180,7 +2192,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
         } else {
             acc = pass(0.0, q, q, RK_DOT);
         }
-        ok = reduce(acc, h);
+        ok = reduce(acc, h, kind_of(0) == RK_DOT ? res_col(mode, j, 1) : -1);
     } else {
         double s = 0.0;
         for (int k = t; k < a.npin; k += WT) s += a.pin[k];
@@ -2197,7 +2209,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
         const int kind = kind_of(p);
         if (mode == RES_MGS && blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
         const double acc = pass(mode == RES_MGS ? h : a.coef * h, i, res_col(mode, j, p + 1), kind);
-        if (kind != RK_NONE) ok = reduce(acc, h);
+        if (kind != RK_NONE) ok = reduce(acc, h, next_dot_col(p));
     }
     if (!ok) return;  // uniform per workgroup; *err is set
     if (mode != RES_MGS) {  // reflections: w back to HBM (RES_HH_UP: h = ||w(j+1:n)||^2)
