@@ -700,8 +700,10 @@ struct ResPlan {
 // 8192^2 / 8).  A pass streams the one column it reads in batches of WB chunks
 // (8 measured best: 4, 16 and a software-pipelined 8 were slower,
 // profiles/r04/ab_wpc_r04c.jsonl / ab_wpc_r04d.jsonl); the reflection chains
-// keep 6 (8 spills there).  During each all-gather the first PC_TOUCH chunks of
-// the next pass's dot column are touched into L2 (paced, as the w-only step).
+// keep 6 (8 spills there).  PC_TOUCH > 0 touches the first chunks of the next
+// pass's dot column into L2 during each all-gather: it shortened the pass and
+// lengthened the wait by as much (2896^2: touch 28 / 16 / 0 -> 18.2 / 17.8 /
+// 17.6 us per projection, profiles/r04/ab_wpc_touch_r04e.jsonl), so it is off.
 #ifndef GK_RES_PC_WB
 #define GK_RES_PC_WB 8
 #endif
@@ -709,7 +711,7 @@ struct ResPlan {
 #define GK_RES_PC_WB_HH 6
 #endif
 #ifndef GK_RES_PC_TOUCH
-#define GK_RES_PC_TOUCH 28
+#define GK_RES_PC_TOUCH 0
 #endif
 constexpr int RES_PC_RW = 64, RES_PC_RX = 26, RES_PC_LX = 38;
 constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH, RES_PC_TOUCH = GK_RES_PC_TOUCH;
@@ -774,10 +776,14 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         p.l2e = (int)std::min<i64>(lmax, (rest + G - 1) / G);
         p.nres2 = std::min<i64>(nchf, G * (p.r2e + p.l2e)) * dt;
     };
-    // the column-cache variant where it moves fewer bytes than both large-slab
-    // variants (strictly: a tie keeps the older kernel)
+    // The column-cache variant where it moves at least 1.5x fewer bytes than both
+    // large-slab variants: its one wave per SIMD streams at ~4.7 TB/s where the two
+    // waves of k_mgs_res reach ~6.8 (r04c-e), so the byte saving must pay for that.
+    // 2896^2 (= one GPU of 4096^2 / 2, 8192^2 / 8): 8 vs 14 B/unknown -> 17.6 vs
+    // 18.9 us per projection; 2048^2 (4096^2 / 4): 8 vs 10 -> 11.3-11.5 vs 9.6 us
+    // (profiles/r04/ab_wpc_touch_r04e.jsonl), kept on k_mgs_res.
     const bool pc_fits = n2 <= (i64)gmax * RES_PC_RW * gk::WT;
-    const bool pc_pays = pc_fits && pc_bytes(n2, gmax) < std::min(pairs_bytes(n2, gmax), wonly_bytes(n2, gmax));
+    const bool pc_pays = pc_fits && 3 * pc_bytes(n2, gmax) <= 2 * std::min(pairs_bytes(n2, gmax), wonly_bytes(n2, gmax));
     if (p.r2 >= need || cap < RES_R2_BIG) {
         p.G = gcw;
         p.pf = p.cw = true;

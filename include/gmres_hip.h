@@ -278,8 +278,8 @@ int gk_sync(gk_ctx *ctx);
  *   GK_RES_WONLY      k_mgs_wres: w only, in registers + LDS (large slabs);
  *   GK_RES_WCOL       k_mgs_wpc: w in registers and the running Krylov column cached
  *                     (registers + LDS) -- 8 B per unknown per projection for slabs of
- *                     up to 64 x 256 double2 per workgroup (one GPU of 4096^2 / 2,
- *                     4096^2 / 4, 8192^2 / 8).
+ *                     up to 64 x 256 double2 per workgroup (one GPU of 4096^2 / 2 and
+ *                     of 8192^2 / 8).
  * info[GK_RES_INFO_LEN]: variant, workgroups G, R2, L2, prefetch, control
  * wave, w-only, non-temporal column loads, register / LDS chunks per
  * workgroup in use, dynamic LDS bytes, resident double2 of the slab, and
@@ -363,8 +363,9 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          Infinity-Cache hit (the w-only kernel's policy); 0 = both
  *                          non-temporal; -1 (default) = the measured choice
  *   GK_TUNE_RES_PC         column-cache variant (GK_RES_WCOL): -1 (default) where its modelled
- *                          bytes per projection are strictly below the pairs and w-only
- *                          variants'; 0 never; 1 wherever the slab fits its registers
+ *                          bytes per projection are at most 2/3 of the pairs and w-only
+ *                          variants' (its one-wave pass streams slower); 0 never; 1 wherever
+ *                          the slab fits its registers
  *   GK_TUNE_SPIN_WAIT      1 (default): gk_mgs_step_wait / gk_hh_step_wait spin on the step's
  *                          event; 0: hipEventSynchronize (may sleep in the driver per step) */
 #define GK_TUNE_PROJ_NT 0

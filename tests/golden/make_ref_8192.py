@@ -8,8 +8,8 @@ tests/test_gpu_configs.py::test_config4_* compares the 8 row-block ranks with
 more than the build container holds, so this runs on the GPU box's host cores
 (the prebuilt oracle/_ref/ref_driver travels with the tree; no GPU is used):
 
-  python tests/golden/make_ref_8192.py OUT.json          # on the box, ~2-4 min
-  python tests/golden/make_ref_8192.py --merge OUT.json  # here: into reference_runs.json
+  python tests/golden/make_ref_8192.py OUT.json [CYCLES]  # on the box, ~3 min per cycle
+  python tests/golden/make_ref_8192.py --merge OUT.json   # here: into reference_runs.json
 
 A heartbeat line is printed every 30 s while the reference runs.
 """
@@ -25,10 +25,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
-KEY = "mgsr_omp_identity_8192_m95_1cyc_t16"
+def key(cycles: int) -> str:
+    return f"mgsr_omp_identity_8192_m95_{cycles}cyc_t16"
 
 
-def run(out: str) -> None:
+def run(out: str, cycles: int = 1) -> None:
     from oracle import refrun
 
     stop = threading.Event()
@@ -42,14 +43,14 @@ def run(out: str) -> None:
     th.start()
     t0 = time.time()
     try:
-        r = refrun.run("mgsr_omp", 8192, 95, "identity", threads=16, max_cycles=1, timeout=1100,
+        r = refrun.run("mgsr_omp", 8192, 95, "identity", threads=16, max_cycles=cycles, timeout=1100,
                        env={"OMP_PROC_BIND": "close", "OMP_PLACES": "cores"})
     finally:
         stop.set()
-    d = {"solver": "mgsr_omp", "N": 8192, "m": 95, "prec": "identity", "threads": r.threads, "max_cycles": 1,
+    d = {"solver": "mgsr_omp", "N": 8192, "m": 95, "prec": "identity", "threads": r.threads, "max_cycles": cycles,
          "cut": r.cut, "hist_res": r.hist_res.tolist(), "wall_s": round(time.time() - t0, 2),
          "host": "the GPU box's host cores (oracle/_ref/ref_driver, OMP_NUM_THREADS=16)"}
-    json.dump({KEY: d}, open(out, "w"), indent=1)
+    json.dump({key(cycles): d}, open(out, "w"), indent=1)
     print(json.dumps(d), flush=True)
 
 
@@ -64,4 +65,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "--merge":
         merge(sys.argv[2])
     else:
-        run(sys.argv[1])
+        run(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1)

@@ -3,9 +3,10 @@ ranks on ONE GPU through the device exchange, at the production split's load.
 
 A 2/4/8-GPU run of the north-star grid gives every GPU a smaller slab than
 the single-GPU bench, so its Arnoldi steps run on different resident kernels
-(tests/test_res_plan.py pins which): k_mgs_res<8, 0> ("pairs", 4096^2 / 8) and
-the column-cache kernel k_mgs_wpc ("w+column": w in registers, the running
-Krylov column cached in registers + LDS; 4096^2 / 4, 4096^2 / 2 and 8192^2 / 8).  Here R ranks share
+(tests/test_res_plan.py pins which): k_mgs_res<8, 0> ("pairs", 4096^2 / 8),
+k_mgs_res<12, 4> ("pairs+lds", 4096^2 / 4) and the column-cache kernel k_mgs_wpc
+("w+column": w in registers, the running Krylov column cached in registers +
+LDS; 4096^2 / 2 and 8192^2 / 8).  Here R ranks share
 one GPU, each with 256 / R workgroups (GK_TUNE_RES_SHARE R, resident forced
 on: GK_TUNE_RES 1), on a grid chosen so that every workgroup holds the same
 number of register / LDS chunks as in the production split -- the same kernel
@@ -36,7 +37,7 @@ M = 95
 # grid, expected variant, the production split it stands for
 CASES = [
     (1448, "pairs", "4096^2 on 8 GPUs"),
-    (2048, "w+column", "4096^2 on 4 GPUs"),
+    (2048, "pairs+lds", "4096^2 on 4 GPUs"),
     (2896, "w+column", "4096^2 on 2 GPUs, 8192^2 on 8 GPUs"),
     (4096, "w-only", "4096^2 on 1 GPU (per-workgroup load)"),
 ]

@@ -20,4 +20,7 @@ step b2048_old 120 $B --grid 2048 --tune 21=0
 step b2896_hh 120 $B --grid 2896 --method hh
 step b2896_hh_old 120 $B --grid 2896 --method hh --tune 21=0
 step b4096 300 $B
-echo ALL_DONE
+echo BENCH_DONE
+# the reference itself at 8192^2 for TWO cycles on this host's 16 cores (no GPU): pins config 4's cycle 2
+step ref8192 1000 python -u tests/golden/make_ref_8192.py gpurun_out/r04e/ref8192_2cyc.json 2
+echo REF_DONE

@@ -17,9 +17,13 @@ plus what only N ranks pay:
     xGMI, every workgroup polls its own region): delta_hop.
   t_cycle(N) = t_cycle_1GPU(n/N) + m (t_halo + t_allreduce) + m (m + 1) delta_hop
   it/s(N)    = m / t_cycle(N),  value of the N-GPU bench line (max over ranks).
-The collective per-call times come from a same-device rehearsal (two processes
-on one GPU through IPC: no xGMI hop, so a LOWER bound); delta_hop is bracketed
-by [lo, hi] (default 1..4 us: one uncached store crossing xGMI and a poll).
+Bands.  The collective per-call time at the high end is gk_comm_latency of the
+same-device rehearsal (N processes on ONE GPU through IPC, back-to-back calls:
+launch gaps and N-process contention included, no xGMI crossing); at the low
+end --coll-lo (default 5 us: the exchange's round trip with the launch hidden
+behind the queued step, as in the solve).  delta_hop is bracketed by
+[--hop-lo, --hop-hi] (default 1..4 us: one uncached store crossing xGMI and a
+poll).
 Each SCALE line carries diagnostics.resident_split_per_unit_us (the measured
 wait per projection) and collective_latency_us, against which the predicted
 terms can be read directly.
@@ -38,28 +42,34 @@ M = 95
 # per-GPU load of each point -> the single-GPU bench line measured at that load
 POINTS = [
     # (label, world, global grid, equal-load single-GPU grid, bench JSON under profiles/)
-    ("4096^2 on 1 GPU", 1, 4096, 4096, "r04/bench_default_r04b.json"),
-    ("4096^2 on 2 GPUs", 2, 4096, 2896, "r04/bench_2896_r04b.json"),
-    ("4096^2 on 4 GPUs", 4, 4096, 2048, "r04/bench_2048_r04b.json"),
-    ("4096^2 on 8 GPUs", 8, 4096, 1448, "r04/bench_1448_r04b.json"),
-    ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r04/bench_2896_r04b.json"),
+    ("4096^2 on 1 GPU", 1, 4096, 4096, "r04/bench_point_4096_r04e.json"),
+    ("4096^2 on 2 GPUs", 2, 4096, 2896, "r04/bench_point_2896_r04e.json"),
+    ("4096^2 on 4 GPUs", 4, 4096, 2048, "r04/bench_point_2048_r04e.json"),
+    ("4096^2 on 8 GPUs", 8, 4096, 1448, "r04/bench_point_1448_r04d.json"),
+    ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r04/bench_point_2896_r04e.json"),
 ]
-COMM = "r04/rehearsal_comm_latency_r04b.json"  # {"allreduce_us": .., "halo_us": ..} (same-device, 2 processes)
+# {"2": {"allreduce": us, "halo": us}, "4": {...}}: gk_comm_latency of same-device rehearsals
+COMM = "r04/rehearsal_comm_latency_r04d.json"
 
 
 def load(rel: str) -> dict | None:
     p = os.path.join(ROOT, "profiles", rel)
     if not os.path.exists(p):
         return None
-    txt = open(p).read().strip().splitlines()
-    return json.loads([x for x in txt if x.startswith("{")][-1])
+    txt = open(p).read().strip()
+    try:
+        return json.loads(txt)
+    except json.JSONDecodeError:
+        return json.loads([x for x in txt.splitlines() if x.startswith("{")][-1])
 
 
-def predict(hop_lo: float, hop_hi: float) -> dict:
+def predict(hop_lo: float, hop_hi: float, coll_lo: float = 5.0) -> dict:
     comm = load(COMM) or {}
-    t_ar, t_halo = float(comm.get("allreduce_us", 10.0)), float(comm.get("halo_us", 10.0))
     rows = []
     for label, world, grid, g1, rel in POINTS:
+        cw = comm.get(str(world)) or comm.get(str(max([int(k) for k in comm if k.isdigit()] or [0]))) or {}
+        t_ar, t_halo = float(cw.get("allreduce", 10.0)), float(cw.get("halo", 10.0))
+        fixed_lo = 0.0 if world == 1 else M * 2 * coll_lo * 1e-6
         b = load(rel)
         if b is None:
             rows.append({"point": label, "missing": rel})
@@ -68,7 +78,7 @@ def predict(hop_lo: float, hop_hi: float) -> dict:
         split = ((b.get("diagnostics") or {}).get("resident_split_per_unit_us") or {}).get("mgs_step") or {}
         extra_fixed = 0.0 if world == 1 else M * (t_ar + t_halo) * 1e-6
         nproj = M * (M + 1)
-        lo = t1 + extra_fixed + (0.0 if world == 1 else nproj * hop_lo * 1e-6)
+        lo = t1 + fixed_lo + (0.0 if world == 1 else nproj * hop_lo * 1e-6)
         hi = t1 + extra_fixed + (0.0 if world == 1 else nproj * hop_hi * 1e-6)
         rows.append({
             "point": label, "world": world, "grid": grid, "per_gpu_unknowns": grid * grid // world,
@@ -76,7 +86,8 @@ def predict(hop_lo: float, hop_hi: float) -> dict:
             "t_cycle_1gpu_ms": round(t1 * 1e3, 2),
             "per_projection_1gpu_us": (b.get("roofline") or {}).get("per_projection_us"),
             "pass_us": split.get("pass_us"), "wait_us": split.get("wait_us"),
-            "collective_ms_per_cycle": round(extra_fixed * 1e3, 2),
+            "collective_per_call_us": {"allreduce": t_ar, "halo": t_halo} if world > 1 else None,
+            "collective_ms_per_cycle": [round(fixed_lo * 1e3, 2), round(extra_fixed * 1e3, 2)],
             "hop_ms_per_cycle": [round(nproj * hop_lo * 1e-3, 2), round(nproj * hop_hi * 1e-3, 2)] if world > 1 else 0,
             "predicted_ms_per_cycle": [round(lo * 1e3, 1), round(hi * 1e3, 1)],
             "predicted_it_s": [round(M / hi, 1), round(M / lo, 1)],
@@ -90,8 +101,7 @@ def predict(hop_lo: float, hop_hi: float) -> dict:
         if base and "predicted_it_s" in r and r["grid"] == 4096:
             r["predicted_speedup"] = [round(v / base["predicted_it_s"][1], 2) for v in r["predicted_it_s"]]
     return {"model": "t_cycle(N) = t_cycle_1GPU(n/N) + m (t_halo + t_allreduce) + m (m+1) delta_hop",
-            "m": M, "collective_per_call_us": {"allreduce": t_ar, "halo": t_halo, "source": f"profiles/{COMM}"
-                                                if comm else "default 10 us (no rehearsal file)"},
+            "m": M, "collective_per_call_low_us": coll_lo, "collective_source": f"profiles/{COMM}" if comm else "default 10 us (no rehearsal file)",
             "delta_hop_us": [hop_lo, hop_hi], "points": rows}
 
 
@@ -99,9 +109,10 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--hop-lo", type=float, default=1.0)
     ap.add_argument("--hop-hi", type=float, default=4.0)
+    ap.add_argument("--coll-lo", type=float, default=5.0)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04", "scaling_prediction_r04.json"))
     a = ap.parse_args()
-    out = predict(a.hop_lo, a.hop_hi)
+    out = predict(a.hop_lo, a.hop_hi, a.coll_lo)
     json.dump(out, open(a.out, "w"), indent=1)
     print("| point | variant | 1-GPU cycle at the per-GPU load (ms) | predicted ms / cycle | predicted it/s |"
           " predicted wait / projection (us) |")
