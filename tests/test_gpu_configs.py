@@ -142,11 +142,12 @@ def test_config4_8192_eight_row_block_ranks_on_one_gpu(transport):
     assert r["comm_launches"] > 0 and r["same_decisions"] and r["n_out"] == 95, r
     if transport == "xchg-res":
         # every Arnoldi step one resident launch per rank, no per-projection launch or
-        # all-reduce call: the all-reduce launches left are one per step (the stencil's
-        # fused first dot) and one each for ||b||, the cycle start's norm and the
-        # true residual of the history
-        assert r["res_G"] == [32] and r["res_launches_min"] >= 95 and r["proj_launches_max"] <= 1, r  # 1: ||b||
-        assert r["comm_launches_max"] <= 95 + 3, r
+        # all-reduce call: the all-reduce launches left are, per cycle, one per step (the
+        # stencil's fused first dot), the cycle start's norm and the history's true
+        # residual, plus ||b|| once per solve (9,120 per cycle on the launch path)
+        cyc = len(r["hist_res"])
+        assert r["res_G"] == [32] and r["res_launches_min"] >= 95 * cyc and r["proj_launches_max"] <= 1, r
+        assert r["comm_launches_max"] <= cyc * (95 + 2) + 1, r
     else:
         assert r["res_launches_min"] == 0, r
     assert r["hist_res0"] == pytest.approx(r["ref_hist_res0"], rel=1e-9), r
