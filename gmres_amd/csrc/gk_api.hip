@@ -161,7 +161,10 @@ struct gk_ctx {
     int tune_res_qdef = -1;   // k_mgs_res NT: V_q of the LDS / streamed parts with the default policy (-1 auto)
     int tune_res_pc = -1;     // column-cache variant k_mgs_wpc: -1 by the byte model, 0 never, 1 where it fits
     std::vector<hipGraphExec_t> gstep;  // captured step j (launch path), valid for partial-slab count gkey
+    std::vector<unsigned> gxs;          // device exchanges in captured step j (their sequence numbers)
     int gkey = -1;
+    unsigned graph_seq0 = 0;            // xs_seq when the capture in progress began
+    unsigned *xs_seqdev = nullptr;      // device: the sequence base of a replayed graph's exchanges
     bool capturing = false;   // a step is being captured: no profiling events inside it
     // tuning knobs (gk_set_tuning)
     int tune_nt = -1, tune_pj_blocks = 0, tune_st_blocks = 0;  // tune_nt: -1 auto
@@ -257,6 +260,7 @@ int xs_alloc(gk_ctx *c) {
         hipSuccess)
         return set_err(GK_ERR_NOMEM, "cannot allocate the exchange region");
     HIPCHK(hipMemsetAsync(c->xs_buf, 0, sizeof(gk::u64) * c->xs_words, c->st));
+    HIPCHK(hipMalloc((void **)&c->xs_seqdev, sizeof(unsigned)));
     HIPCHK(hipHostMalloc((void **)&c->xs_err, sizeof(int), hipHostMallocMapped));
     HIPCHK(hipHostGetDevicePointer((void **)&c->xs_err_dev, c->xs_err, 0));
     *c->xs_err = 0;
@@ -358,19 +362,24 @@ int sync_st(gk_ctx *c) {
 }
 
 int xs_exchange(gk_ctx *c, double *buf, int count, int mode, int root) {
-    const unsigned seq = ++c->xs_seq;
+    unsigned seq = ++c->xs_seq;
+    const unsigned *base = nullptr;
+    if (c->capturing) {  // a graph node: its number relative to the base set before each replay
+        seq -= c->graph_seq0;
+        base = c->xs_seqdev;
+    }
     switch (mode) {
         case gk::XS_SLAB:
-            gk::k_xchg<gk::XS_SLAB><<<1, gk::TPB, 0, c->st>>>(buf, count, c->xs_peers, c->nranks, c->rank, seq, root,
-                                                            c->xs_err_dev, c->xs_timeout);
+            gk::k_xchg<gk::XS_SLAB><<<1, gk::TPB, 0, c->st>>>(buf, count, c->xs_peers, c->nranks, c->rank, seq, base,
+                                                            root, c->xs_err_dev, c->xs_timeout);
             break;
         case gk::XS_VEC:
-            gk::k_xchg<gk::XS_VEC><<<1, gk::TPB, 0, c->st>>>(buf, count, c->xs_peers, c->nranks, c->rank, seq, root,
-                                                           c->xs_err_dev, c->xs_timeout);
+            gk::k_xchg<gk::XS_VEC><<<1, gk::TPB, 0, c->st>>>(buf, count, c->xs_peers, c->nranks, c->rank, seq, base,
+                                                           root, c->xs_err_dev, c->xs_timeout);
             break;
         default:
             gk::k_xchg<gk::XS_BCAST><<<1, gk::TPB, 0, c->st>>>(buf, count, c->xs_peers, c->nranks, c->rank, seq,
-                                                             root, c->xs_err_dev, c->xs_timeout);
+                                                             base, root, c->xs_err_dev, c->xs_timeout);
             break;
     }
     LAUNCHCHK();
@@ -1441,8 +1450,13 @@ int mgs_chain(gk_ctx *c, int j, int np) {
 int capture_step(gk_ctx *c, int j, int np) {
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
     c->capturing = true;
+    c->graph_seq0 = c->xs_seq;
     const int rc = mgs_chain(c, j, np);
     c->capturing = false;
+    const unsigned nxs = c->xs_seq - c->graph_seq0;  // nothing ran: the numbers are reused by the replay
+    c->xs_seq = c->graph_seq0;
+    if ((int)c->gxs.size() < c->m + 1) c->gxs.resize(c->m + 1, 0);
+    c->gxs[j] = nxs;
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(c->st, &g);
     hipGraphExec_t ge = nullptr;
@@ -1575,6 +1589,7 @@ int gk_destroy(gk_ctx *c) {
     if (c->lscratch) (void)hipFree(c->lscratch);
     for (void *p : c->xs_mapped) (void)hipIpcCloseMemHandle(p);
     if (c->xs_buf) (void)hipFree(c->xs_buf);
+    if (c->xs_seqdev) (void)hipFree(c->xs_seqdev);
     if (c->xs_err) (void)hipHostFree(c->xs_err);
     if (c->res_gath) (void)hipFree(c->res_gath);
     if (c->res_stamps) (void)hipFree(c->res_stamps);
@@ -2068,7 +2083,7 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
     }
     // Launch path: RCCL ranks (or one rank with the resident step off) replay the
     // step's projection chain as a hipGraph captured at its first use (GK_TUNE_GRAPH).
-    if (c->tune_graph && !c->tune_rev && !c->xs_on && c->lg == nullptr) {
+    if (c->tune_graph && !c->tune_rev && (c->lg == nullptr || c->xs_on)) {
         if (c->gkey != np) {
             graph_reset(c);
             c->gkey = np;
@@ -2078,6 +2093,10 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
         if (c->gstep[j] != nullptr) {
             {
                 ProfScope ps(c, GK_KID_GRAPH);
+                if (c->xs_on && c->gxs[j] > 0) {  // the replay's exchanges continue this context's numbering
+                    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->xs_seqdev), (int)c->xs_seq, 1, c->st));
+                    c->xs_seq += c->gxs[j];
+                }
                 HIPCHK(hipGraphLaunch(c->gstep[j], c->st));
             }
             HIPCHK(hipEventRecord(c->ev_step[j], c->st));

@@ -718,9 +718,14 @@ __device__ __forceinline__ void xs_fail(int *err, int op, int src) {
 //   XS_BCAST: buf = root's buf, count <= XS_MAXV.
 // The rank-order sum is the same instruction sequence on every rank, so the
 // replicated host loops see bit-identical scalars.
+// seqbase != nullptr (a launch replayed from a captured graph): the sequence
+// number is *seqbase + seq, the host having set *seqbase on the stream before the
+// replay -- a graph's kernel arguments are fixed, an exchange's number is not.
 template <int MODE>
 __global__ __launch_bounds__(TPB) void k_xchg(double *__restrict__ buf, int count, XsPeers peers, int nranks,
-                                               int rank, unsigned seq, int root, int *err, u64 timeout) {
+                                               int rank, unsigned seq_arg, const unsigned *seqbase, int root,
+                                               int *err, u64 timeout) {
+    const unsigned seq = seqbase != nullptr ? *seqbase + seq_arg : seq_arg;
     __shared__ double sm[WAVES];
     __shared__ double pay[XS_MAXV];
     __shared__ unsigned rv[XS_MAXR * XS_MAXV * 2];
@@ -1597,6 +1602,17 @@ constexpr int TOUCH_PACE = GK_RES_TOUCH_PACE;
 // the reflection chains' pacing (0 = burst); re-measured after the depth / residency
 // re-tune (profiles/r02/ab_pace_retune.jsonl): 8 / 24 -> 41.06 / 41.1 vs 40.57 us burst
 constexpr int TOUCH_PACE_HH = GK_RES_TOUCH_PACE_HH;
+#ifndef GK_RES_REV
+#define GK_RES_REV 0
+#endif
+// REV (A/B knob): the LDS part of a workgroup's chunks is split into halves lo /
+// hi; even passes walk lo, registers, hi and odd passes hi, registers, lo, so a
+// pass's AXPY column V_i -- the previous pass's dot column -- starts with the
+// half that pass read last, on lines still in L2 (a half: 19 chunks of 4 KiB
+// per column, inside a workgroup's 128 KiB share of its XCD's L2).  The register
+// part keeps one order (a second unrolled order spills).  The touch of the next
+// dot column covers the half the next pass starts with.
+constexpr bool RES_REV = GK_RES_REV != 0;
 
 // STEN (RES_MGS, identity operator): the launch forms w = A V(:,j) in its
 // prologue -- the stencil launch's arithmetic, ((W+E)+N)+S and 4x - s, element
@@ -1735,19 +1751,18 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     };
     // One pass over the slab: w -= ch V_i, then the reduction `kind`
     // (<w, V_q>, ||w(tail0:)||^2, or none).  Returns this thread's partial.
-    auto pass = [&](double ch, int i, int q, int kind) -> double {
+    auto pass = [&](double ch, int i, int q, int kind, bool rev) -> double {
         const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
         const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
         const bool dot = kind == RK_DOT;
         double acc = 0.0;
-        // registers: batches of WBT chunks, both columns in flight
-#pragma unroll
-        for (int k0 = 0; k0 < RW; k0 += WBT) {
+        // registers: batches of WBT chunks, both columns in flight (k0 a constant once unrolled)
+        auto rbatch = [&](const int k0) {
             double2 av[WBT], bv[WBT];
 #pragma unroll
             for (int u = 0; u < WBT; ++u) {
                 const i64 c = c0 + k0 + u;
-                if (XPF && k0 == 0 && xpf_wave) {
+                if (XPF && k0 == 0 && xpf_wave && !rev) {
                     av[u] = pa[u];
                     bv[u] = pb[u];
                 } else if (k0 + u < RW && c < cend) {
@@ -1764,14 +1779,14 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                     red(acc, wr[k], bv[u], kind, (c0 + k) * WT + t, mode == RES_HH_UP && c0 + k == 0);
                 }
             }
-        }
+        };
         // LDS: the same, w from / to LDS
-        for (int k0 = 0; k0 < LW; k0 += WBT) {
+        auto lbatch = [&](const int k0, const int kend) {
             double2 av[WBT], bv[WBT];
 #pragma unroll
             for (int u = 0; u < WBT; ++u) {
                 const i64 c = l0 + k0 + u;
-                if (k0 + u < LW && c < lend) {
+                if (k0 + u < kend && c < lend) {
                     av[u] = ldv<true>(A2 + c * WT + t);
                     if (dot) bv[u] = ldv<RES_QNT>(B2 + c * WT + t);
                 }
@@ -1779,7 +1794,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 #pragma unroll
             for (int u = 0; u < WBT; ++u) {
                 const int k = k0 + u;
-                if (k < LW && l0 + k < lend) {
+                if (k < kend && l0 + k < lend) {
                     double2 wv = lw[k * WT + t];
                     wv.x = wv.x - ch * av[u].x;
                     wv.y = wv.y - ch * av[u].y;
@@ -1787,7 +1802,14 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                     red(acc, wv, bv[u], kind, (l0 + k) * WT + t, mode == RES_HH_UP && l0 + k == 0);
                 }
             }
-        }
+        };
+        constexpr int LH = RES_REV ? LW / 2 : 0;  // LDS halves [0, LH) and [LH, LW)
+        const int f0 = rev ? LH : 0, f1 = rev ? LW : LH;  // the half walked first
+        for (int k0 = f0; k0 < f1; k0 += WBT) lbatch(k0, f1);
+#pragma unroll
+        for (int k0 = 0; k0 < RW; k0 += WBT) rbatch(k0);
+        const int s0 = rev ? 0 : LH, s1 = rev ? LH : LW;  // and last
+        for (int k0 = s0; k0 < s1; k0 += WBT) lbatch(k0, s1);
         for (i64 e0 = sbase; e0 < n2; e0 += 2 * sstride) {  // streamed part: 32 B/unknown
             double2 wv[2], av[2], bv[2];
 #pragma unroll
@@ -1821,7 +1843,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     };
     // all-gather of the partials: the same h in every workgroup (and rank)
     int xi = 0;
-    auto reduce = [&](double acc, double &h, int touch_col) -> bool {
+    auto reduce = [&](double acc, double &h, int touch_col, bool trev = false) -> bool {
         clk.passed(a.stamps);
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
@@ -1835,8 +1857,14 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 // lines [0, 32*TCH) of the workgroup's register-resident part of
                 // the column (contiguous from chunk c0); all loads land in one sink
                 // register, drained below before anything can reuse it
-                const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + c0 * WT);
-                const i64 lines = (i64)32 * (cend - c0 < TCH ? (cend - c0 > 0 ? cend - c0 : 0) : TCH);
+                // (REV: the LDS half the next pass starts with)
+                i64 r0 = c0, r1 = cend;
+                if constexpr (RES_REV) {
+                    r0 = trev ? l0 + LW / 2 : l0;
+                    r1 = trev ? lend : (l0 + LW / 2 < lend ? l0 + LW / 2 : lend);
+                }
+                const i64 lines = (i64)32 * (r1 - r0 < TCH ? (r1 - r0 > 0 ? r1 - r0 : 0) : TCH);
+                const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + r0 * WT);
                 for (i64 l = t - 64; l < lines; l += WT - 64) {
                     if constexpr (PACE > 0) {
                         if (*(volatile int *)&xdone) break;  // wave-uniform: one LDS word
@@ -1859,6 +1887,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     // back from, so the pass code of all three modes is the same (the tail test
     // inside the unrolled loop made the UP pass 28 % slower: 45.9 vs 35.7 us).
     auto kind_of = [&](int p) { return p < np - 1 ? RK_DOT : (mode == RES_MGS ? RK_NORM : RK_NONE); };
+    auto rev_of = [&](int p) { return RES_REV && (p & 1) != 0; };
     double h;
     bool ok = true;
     if (mode == RES_HH_DOWN) {
@@ -1870,7 +1899,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         if (a.unit_known) {  // <e_u, P_q> = P_q(u): the one nonzero product, as the full sum gives it
             if (blockIdx.x == 0 && t == 0 && a.unit_e >= 0) acc = a.V[(i64)q * a.ld + a.unit_e];
         } else {
-            acc = pass(0.0, q, q, RK_DOT);
+            acc = pass(0.0, q, q, RK_DOT, false);
         }
         if (XPF) load_first(q, res_col(mode, j, 1), kind_of(0) == RK_DOT);
         ok = reduce(acc, h, kind_of(0) == RK_DOT ? res_col(mode, j, 1) : -1);
@@ -1893,9 +1922,11 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         const int i = res_col(mode, j, p);
         const int kind = kind_of(p);
         if (mode == RES_MGS && blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
-        const double acc = pass(mode == RES_MGS ? h : a.coef * h, i, res_col(mode, j, p + 1), kind);
-        if (XPF && p + 1 < np) load_first(res_col(mode, j, p + 1), res_col(mode, j, p + 2), kind_of(p + 1) == RK_DOT);
-        if (kind != RK_NONE) ok = reduce(acc, h, p + 1 < np && kind_of(p + 1) == RK_DOT ? res_col(mode, j, p + 2) : -1);
+        const double acc = pass(mode == RES_MGS ? h : a.coef * h, i, res_col(mode, j, p + 1), kind, rev_of(p));
+        if (XPF && p + 1 < np && !rev_of(p + 1))
+            load_first(res_col(mode, j, p + 1), res_col(mode, j, p + 2), kind_of(p + 1) == RK_DOT);
+        if (kind != RK_NONE)
+            ok = reduce(acc, h, p + 1 < np && kind_of(p + 1) == RK_DOT ? res_col(mode, j, p + 2) : -1, rev_of(p + 1));
     }
     if (!ok) return;  // uniform per workgroup; *err is set
     const bool close = mode == RES_HH_UP && a.close_hh;

@@ -351,10 +351,12 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          and takes the first dot with it (no stencil launch; even N) -- measured
  *                          4 % slower at 4096^2: the prologue's loads cannot be kept in flight beside
  *                          the register-resident w
- *   GK_TUNE_GRAPH          1 (default): a launch-path MGS-R step (RCCL ranks, or one rank with the
- *                          resident step off) is captured once per step index j as a hipGraph --
- *                          its 2j projection launches, 2j + 1 all-reduces (ncclAllReduce captured
- *                          as graph nodes) and the normalisation -- and replayed in later cycles;
+ *   GK_TUNE_GRAPH          1 (default): a launch-path MGS-R step (RCCL ranks, device-exchange ranks
+ *                          with the resident step off, or one rank with it off) is captured once
+ *                          per step index j as a hipGraph -- its 2j projection launches, 2j + 1
+ *                          all-reduces (ncclAllReduce / k_xchg captured as graph nodes; a replayed
+ *                          k_xchg takes its sequence number from a device base set before each
+ *                          replay) and the normalisation -- and replayed in later cycles;
  *                          0: launched call by call.  A capture that fails switches it off for
  *                          the context (gk_last_error keeps the reason).
  *   GK_TUNE_RES_QDEF       k_mgs_res with non-temporal columns (pairs / pairs+lds): 1 = the LDS-held

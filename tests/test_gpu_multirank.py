@@ -186,6 +186,72 @@ def test_launch_path_step_graphs(monkeypatch, rccl):
           f"{t1 / cyc * 1e3:.2f} ms/cycle replayed graphs")
 
 
+@pytest.mark.parametrize("R", [2, 3])
+def test_launch_path_step_graphs_device_exchange(R):
+    """GK_TUNE_GRAPH over the device exchange (in-process slab ranks, resident
+    kernels off): the captured step's k_xchg launches read their sequence
+    numbers from a device base the host sets before every replay, so replayed
+    graphs keep the exchange's numbering -- results equal the call-by-call run
+    bit for bit on every rank, and every Arnoldi step ran as a replay."""
+    import time
+
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+
+    N, m, cyc = 256, 30, 4
+    parts = ga.slab_partition(N, R)
+    runs = {}
+    for graph in (0, 1):
+        g = ga.LocalGroup(R)
+        ctxs = [ga.Context(N, m, device=0, line0=l0, nlines=nl) for l0, nl in parts]
+        out, err = [None] * R, []
+        try:
+            for r, c in enumerate(ctxs):
+                c.comm_init_local(g, r, max(nl for _, nl in parts))
+            for c in ctxs:
+                c.xchg_local()
+                c.tune(nat.GK_TUNE_RES, 0)
+                c.tune(nat.GK_TUNE_GRAPH, graph)
+
+            def work(r):
+                try:
+                    c = ctxs[r]
+                    c.set_rhs_ones()
+                    ga.gmres_mgsr(c, 1e-15, max_cycles=1, want_verr=False)  # graphs captured here
+                    c.profile(True)
+                    c.profile_reset()
+                    c.sync()
+                    t0 = time.perf_counter()
+                    res = ga.gmres_mgsr(c, 1e-15, max_cycles=cyc, want_hist=True, want_verr=False)
+                    c.sync()
+                    out[r] = (res, c.profile_read(), time.perf_counter() - t0)
+                except Exception as e:  # pragma: no cover - reported below
+                    err.append(e)
+
+            th = [threading.Thread(target=work, args=(r,)) for r in range(R)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(timeout=100)
+            assert not err, err
+            assert all(o is not None for o in out)
+            runs[graph] = out
+        finally:
+            for c in ctxs:
+                c.close()
+            g.close()
+    for r in range(R):
+        r0, p0, _ = runs[0][r]
+        r1, p1, _ = runs[1][r]
+        assert np.array_equal(r0.hist_res, r1.hist_res) and np.array_equal(r0.x, r1.x)
+        assert p1["graph"][1] == cyc * m and p1["proj"][1] <= 1, p1
+        assert p0["graph"][1] == 0 and p0["proj"][1] > 0, p0
+    t0 = max(o[2] for o in runs[0]) / cyc * 1e3
+    t1 = max(o[2] for o in runs[1]) / cyc * 1e3
+    print(f"launch path, device exchange, {R} ranks {N}^2 m={m}: {t0:.2f} ms/cycle call by call, "
+          f"{t1:.2f} ms/cycle replayed graphs")
+
+
 @pytest.mark.parametrize("N,nranks", [(66, 3), (20, 4), (16, 5), (130, 2)])
 @pytest.mark.parametrize("degree", [1, 3, 4, 6, 8])
 def test_chebyshev_on_slabs_bitexact(oracle, N, nranks, degree):
