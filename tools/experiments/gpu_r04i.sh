@@ -2,7 +2,8 @@
 # group's contexts now replay too), then an A/B of k_mgs_wres pass ordering at
 # 4096^2: REV (LDS halves walked lo/regs/hi then hi/regs/lo, so a pass's AXPY
 # column starts on the lines the previous pass read last) with the touch depth
-# 28 (capped at a half, 19) / 8 / 0, against the default, MGS-R and Householder.
+# 28 (capped at a half, 19) / 8 / 0, against the default, MGS-R and Householder;
+# the column-cache kernel's batch depth 12 / 10 vs 8 at 2896^2.
 OUT=gpurun_out/r04i
 source tools/gpu_lib.sh
 T="python -u -m pytest -v --timeout 200 --timeout-method thread -p no:cacheprovider"
@@ -17,4 +18,9 @@ step base_b 120 $B
 step rev1_b 120 env GK_LIB_DIR=$V/rev1 $B
 step hh_base 120 $B --method hh
 step hh_rev1 120 env GK_LIB_DIR=$V/rev1 $B --method hh
+step pc_base_a 120 $B --grid 2896
+step pc_wb12 120 env GK_LIB_DIR=$V/pcwb12 $B --grid 2896
+step pc_wb10 120 env GK_LIB_DIR=$V/pcwb10 $B --grid 2896
+step pc_base_b 120 $B --grid 2896
+step pc_wb12_b 120 env GK_LIB_DIR=$V/pcwb12 $B --grid 2896
 echo ALL_DONE
