@@ -72,9 +72,11 @@ def res_regions(plan: dict, nloc: int) -> dict:
     and the w+column variant's cached chunks), unknowns whose w alone is on chip
     (registers of the w-only variant, or LDS), and the streamed rest.  Chunks of
     DT double2: 256 (w-only, w+column), 448 (prefetch, one control wave), 512
-    (pairs)."""
+    (pairs); w+column: the plan's "wt" (512 since round 4's two-wave build)."""
     n2 = nloc // 2
     dt = 256 if plan["variant"] in ("w-only", "w+column") else (448 if plan.get("cw") else 512)
+    if plan["variant"] in ("w-only", "w+column") and plan.get("wt"):
+        dt = int(plan["wt"])  # threads per workgroup = double2 per chunk
     nres2 = min(int(plan["nres2"]), n2)
     nreg2 = min(nres2, int(plan["G"]) * int(plan["r2e"]) * dt)
     if plan["variant"] == "w-only":

@@ -699,6 +699,7 @@ struct ResPlan {
     int r2e = 0, l2e = 0;  // chunks per workgroup used: the resident prefix spread evenly over G
     bool pf = false, nt = false, cw = false, wo = false;
     bool pc = false;       // column-cache variant (k_mgs_wpc): w in registers, running column cached
+    int wt = 0;            // threads per workgroup = double2 per chunk (set by plan_resident)
     i64 nres2 = 0;
     int lds = 0;
 };
@@ -722,7 +723,18 @@ struct ResPlan {
 #ifndef GK_RES_PC_TOUCH
 #define GK_RES_PC_TOUCH 0
 #endif
-constexpr int RES_PC_RW = 64, RES_PC_RX = 26, RES_PC_LX = 38;
+// PC_NT: threads per workgroup -- 512 (two waves per SIMD: one consumes a batch
+// while the other's loads are in flight) holds the same 64 x 256 double2 of w per
+// workgroup as 256 threads x 64 chunks, at 32 chunks per thread.
+#ifndef GK_RES_PC_NT
+#define GK_RES_PC_NT 256
+#endif
+constexpr int RES_PC_NT = GK_RES_PC_NT;
+static_assert(RES_PC_NT == 256 || RES_PC_NT == 512, "column-cache workgroups of one or two waves per SIMD");
+#ifndef GK_RES_PC_RX
+#define GK_RES_PC_RX (RES_PC_NT == 512 ? 13 : 26)
+#endif
+constexpr int RES_PC_RW = RES_PC_NT == 512 ? 32 : 64, RES_PC_RX = GK_RES_PC_RX, RES_PC_LX = RES_PC_NT == 512 ? 19 : 38;
 constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH, RES_PC_TOUCH = GK_RES_PC_TOUCH;
 
 // Modelled bytes per projection of a slab of n2 double2 on G workgroups (the
@@ -731,7 +743,7 @@ constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH, RES_PC_T
 // column-cache variant: the cached pairs, the rest of the register-held w, the
 // streamed rest.
 i64 pc_bytes(i64 n2, int G) {
-    const i64 cap = (i64)G * RES_PC_RW * gk::WT, cached = (i64)G * (RES_PC_RX + RES_PC_LX) * gk::WT;
+    const i64 cap = (i64)G * RES_PC_RW * RES_PC_NT, cached = (i64)G * (RES_PC_RX + RES_PC_LX) * RES_PC_NT;
     const i64 r = std::min(n2, cap), c = std::min(r, cached);
     return 8 * c + 16 * (r - c) + 32 * (n2 - r);
 }
@@ -791,7 +803,7 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
     // 2896^2 (= one GPU of 4096^2 / 2, 8192^2 / 8): 8 vs 14 B/unknown -> 17.6 vs
     // 18.9 us per projection; 2048^2 (4096^2 / 4): 8 vs 10 -> 11.3-11.5 vs 9.6 us
     // (profiles/r04/ab_wpc_touch_r04e.jsonl), kept on k_mgs_res.
-    const bool pc_fits = n2 <= (i64)gmax * RES_PC_RW * gk::WT;
+    const bool pc_fits = n2 <= (i64)gmax * RES_PC_RW * RES_PC_NT;
     const bool pc_pays = pc_fits && 3 * pc_bytes(n2, gmax) <= 2 * std::min(pairs_bytes(n2, gmax), wonly_bytes(n2, gmax));
     if (p.r2 >= need || cap < RES_R2_BIG) {
         p.G = gcw;
@@ -803,14 +815,16 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         p.pc = true;
         p.r2 = RES_PC_RX;
         p.l2 = RES_PC_LX;
-        spread(gk::WT, RES_PC_RW, 0);
-        p.lds = RES_PC_LX * gk::WT * (int)sizeof(double2);
+        p.wt = RES_PC_NT;
+        spread(RES_PC_NT, RES_PC_RW, 0);
+        p.lds = RES_PC_LX * RES_PC_NT * (int)sizeof(double2);
         p.nt = true;
         return;
     } else if (tune_wonly > 0 || (tune_wonly < 0 && wonly_pays(n2, gmax))) {
         // w only, one wave per SIMD: 16 B/unknown per projection for ~100 chunks per workgroup
         p.G = gmax;
         p.wo = true;
+        p.wt = gk::WT;
         p.r2 = 0;  // (the kernel's register part is RES_RW / RES_RW_HH chunks: r2e)
         spread(gk::WT, hh ? RES_RW_HH : RES_RW, RES_LW);
         p.lds = RES_LW * gk::WT * (int)sizeof(double2);
@@ -824,6 +838,7 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         spread(dt, RES_R2_BIG, p.l2);
     }
     p.lds = std::max<int>(RES_LDS_MIN, p.l2 * (p.cw ? gk::RT - 64 : gk::RT) * (int)sizeof(double2));
+    p.wt = gk::RT;
     p.nt = nt;
 }
 
@@ -851,7 +866,7 @@ bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
 
 // gk_res_plan_query / gk_res_info layout
 enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, RPI_R2E, RPI_L2E, RPI_LDS, RPI_NRES2, RPI_STEN,
-       RPI_CHEB_STEN };
+       RPI_CHEB_STEN, RPI_WT };
 void plan_info(const ResPlan &p, bool on, long long *info) {
     for (int k = 0; k < GK_RES_INFO_LEN; ++k) info[k] = 0;
     if (!on) return;
@@ -868,6 +883,7 @@ void plan_info(const ResPlan &p, bool on, long long *info) {
     info[RPI_L2E] = p.l2e;
     info[RPI_LDS] = p.lds;
     info[RPI_NRES2] = p.nres2;
+    info[RPI_WT] = p.wt;
 }
 
 // hipFuncSetAttribute is per device: remember the dynamic-LDS size set on each.
@@ -929,11 +945,13 @@ int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
     if (attr[c->dev].load() < p.lds) {
         HIPCHK(hipFuncSetAttribute(
-            reinterpret_cast<const void *>(&gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT, RES_PC_TOUCH>),
+            reinterpret_cast<const void *>(
+                &gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT, RES_PC_TOUCH, RES_PC_NT>),
             hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
         attr[c->dev] = p.lds;
     }
-    gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT, RES_PC_TOUCH><<<p.G, gk::WT, p.lds, c->st>>>(a);
+    gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT, RES_PC_TOUCH, RES_PC_NT>
+        <<<p.G, RES_PC_NT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
 }

@@ -2046,8 +2046,10 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 
 
 // --------------------------------------------------------------------------
-// Resident MGS-R step, column-cache variant (k_mgs_wres's structure: ONE wave
-// per SIMD, 256-thread workgroups, one per CU): w wholly in registers (RW
+// Resident MGS-R step, column-cache variant (k_mgs_wres's structure, NT-thread
+// workgroups, one per CU: NT = 256 one wave per SIMD, 512 two -- the second wave
+// keeps a batch of loads in flight while the first consumes its own, at half
+// the registers per thread): w wholly in registers (RW
 // double2 per thread) and the running Krylov column cached on chip -- RX
 // double2 per thread in registers, LX more in LDS.  A pass reads only its dot
 // column V_q (its AXPY column V_i is the previous pass's V_q, still cached):
@@ -2059,12 +2061,12 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 // k_mgs_res / k_mgs_wres; only the dot summation order within a thread
 // differs.  Columns non-temporal (nothing is re-read through the caches).
 // --------------------------------------------------------------------------
-template <int RW, int RX, int LX, int MODE, int WBT = 8, int TCHP = 0>
-__global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
+template <int RW, int RX, int LX, int MODE, int WBT = 8, int TCHP = 0, int NT = WT>
+__global__ __launch_bounds__(NT, 1) void k_mgs_wpc(ResArgs a) {
     static_assert(RX <= RW && RX + LX <= RW, "the column cache covers register chunks of w only");
-    extern __shared__ double2 lx[];  // [LX][WT]: cached column of chunks RX .. RX + LX - 1
+    extern __shared__ double2 lx[];  // [LX][NT]: cached column of chunks RX .. RX + LX - 1
     __shared__ int xdone;            // the exchange in progress has completed (stops the touches)
-    __shared__ double sm[WT / 64];
+    __shared__ double sm[NT / 64];
     __shared__ double bc[1];
     __shared__ int okf;
     __shared__ double hsh[RHMAX + 1];
@@ -2072,24 +2074,24 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
     constexpr int mode = MODE;
     const int j = a.j, np = res_np(mode, j);
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
-    const i64 nch = a.nres2 / WT;
+    const i64 nch = a.nres2 / NT;
     const i64 c0 = (i64)blockIdx.x * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
     const i64 tail0 = mode == RES_HH_UP ? a.tail0 : 0;
     const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
     double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
     ResClock clk;
     clk.start(a.stamps);
-    const i64 sstride = (i64)gridDim.x * WT;
-    const i64 sbase = a.nres2 + (i64)blockIdx.x * WT + t;
+    const i64 sstride = (i64)gridDim.x * NT;
+    const i64 sbase = a.nres2 + (i64)blockIdx.x * NT + t;
     double2 wr[RW], xc[RX > 0 ? RX : 1];
     {  // w, and the AXPY column of pass 0 into the cache
         const double2 *__restrict__ C2 = V2 + (i64)res_col(mode, j, 0) * ld2;
 #pragma unroll
-        for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
+        for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? W2[(c0 + k) * NT + t] : double2{0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < RX; ++k) xc[k] = (c0 + k < cend) ? ldv<true>(C2 + (c0 + k) * WT + t) : double2{0.0, 0.0};
+        for (int k = 0; k < RX; ++k) xc[k] = (c0 + k < cend) ? ldv<true>(C2 + (c0 + k) * NT + t) : double2{0.0, 0.0};
         for (int k = 0; k < LX; ++k)
-            if (c0 + RX + k < cend) lx[k * WT + t] = ldv<true>(C2 + (c0 + RX + k) * WT + t);
+            if (c0 + RX + k < cend) lx[k * NT + t] = ldv<true>(C2 + (c0 + RX + k) * NT + t);
     }
     // One pass: w -= ch V_i (the cached column; V_i from HBM past the cache), then
     // the reduction `kind`; with a dot, V_q replaces the cached column.  Batches of
@@ -2109,8 +2111,8 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
                 const int k = k0 + u;
                 const i64 c = c0 + k;
                 if (k < RW && c < cend) {
-                    if (dot) bv[u] = ldv<true>(B2 + c * WT + t);
-                    if (k >= RX + LX) av[u] = ldv<true>(A2 + c * WT + t);  // not cached
+                    if (dot) bv[u] = ldv<true>(B2 + c * NT + t);
+                    if (k >= RX + LX) av[u] = ldv<true>(A2 + c * NT + t);  // not cached
                 }
             }
 #pragma unroll
@@ -2121,7 +2123,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
                     if (k < RX)
                         x = xc[k < RX ? k : 0];
                     else if (k < RX + LX)
-                        x = lx[(k - RX) * WT + t];
+                        x = lx[(k - RX) * NT + t];
                     else
                         x = av[u];
                     wr[k].x = wr[k].x - ch * x.x;
@@ -2132,9 +2134,9 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
                         if (k < RX)
                             xc[k < RX ? k : 0] = bv[u];
                         else if (k < RX + LX)
-                            lx[(k - RX) * WT + t] = bv[u];
+                            lx[(k - RX) * NT + t] = bv[u];
                     } else if (kind == RK_NORM) {
-                        sq_acc(acc, wr[k], (c0 + k) * WT + t, tail0, mode == RES_HH_UP && c0 + k == 0);
+                        sq_acc(acc, wr[k], (c0 + k) * NT + t, tail0, mode == RES_HH_UP && c0 + k == 0);
                     }
                 }
             }
@@ -2189,13 +2191,13 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
         if (t == 0) xdone = 0;
         __syncthreads();
         if (t < 64) {
-            res_exchange<WT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
+            res_exchange<NT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
             if (t == 0) *(volatile int *)&xdone = 1;
         } else if constexpr (TCHP > 0) {
             if (touch_col >= 0) {
-                const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + c0 * WT);
+                const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + c0 * NT);
                 const i64 nc = cend - c0 < TCHP ? (cend - c0 > 0 ? cend - c0 : 0) : TCHP;
-                for (i64 l = t - 64; l < 32 * nc; l += WT - 64) {
+                for (i64 l = t - 64; l < 32 * nc; l += NT - 64) {
                     if (*(volatile int *)&xdone) break;  // wave-uniform: one LDS word
                     asm volatile("global_load_dword %0, %1, off" : "+v"(touch_sink) : "v"(base + l * 128) : "memory");
                     __builtin_amdgcn_s_sleep(TOUCH_PACE);
@@ -2226,13 +2228,13 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
         ok = reduce(acc, h, kind_of(0) == RK_DOT ? res_col(mode, j, 1) : -1);
     } else {
         double s = 0.0;
-        for (int k = t; k < a.npin; k += WT) s += a.pin[k];
+        for (int k = t; k < a.npin; k += NT) s += a.pin[k];
         s = wave_sum(s);
         if ((t & 63) == 0) sm[t >> 6] = s;
         __syncthreads();
         h = sm[0];
 #pragma unroll
-        for (int w = 1; w < WT / 64; ++w) h += sm[w];
+        for (int w = 1; w < NT / 64; ++w) h += sm[w];
         __syncthreads();
     }
     for (int p = 0; p < np && ok; ++p) {
@@ -2246,7 +2248,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
     if (mode != RES_MGS) {  // reflections: w back to HBM (RES_HH_UP: h = ||w(j+1:n)||^2)
 #pragma unroll
         for (int k = 0; k < RW; ++k)
-            if (c0 + k < cend) W2[(c0 + k) * WT + t] = wr[k];
+            if (c0 + k < cend) W2[(c0 + k) * NT + t] = wr[k];
         if (mode == RES_HH_UP && blockIdx.x == 0 && t == 0) a.hs[0] = h;
         clk.finish(a.stamps, mode);
         return;
@@ -2256,7 +2258,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
 #pragma unroll
     for (int k = 0; k < RW; ++k)
         if (c0 + k < cend)
-            O2[(c0 + k) * WT + t] = hn != 0.0 ? double2{wr[k].x / hn, wr[k].y / hn} : double2{0.0, 0.0};
+            O2[(c0 + k) * NT + t] = hn != 0.0 ? double2{wr[k].x / hn, wr[k].y / hn} : double2{0.0, 0.0};
     for (i64 e = sbase; e < n2; e += sstride) {
         const double2 v = W2[e];
         O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
@@ -2265,7 +2267,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wpc(ResArgs a) {
     clk.finish(a.stamps, mode);
     if (blockIdx.x == 0) {
         __syncthreads();
-        for (int k = t; k < j; k += WT) {
+        for (int k = t; k < j; k += NT) {
             a.hs[k] = hsh[k];
             a.hcopy[k] = hsh[k];
         }

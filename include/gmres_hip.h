@@ -279,14 +279,14 @@ int gk_sync(gk_ctx *ctx);
  *   GK_RES_WCOL       k_mgs_wpc: w in registers and the running Krylov column cached
  *                     (registers + LDS) -- 8 B per unknown per projection for slabs of
  *                     up to 64 x 256 double2 per workgroup (one GPU of 4096^2 / 2 and
- *                     of 8192^2 / 8).
+ *                     of 8192^2 / 8), in 512-thread workgroups (two waves per SIMD).
  * info[GK_RES_INFO_LEN]: variant, workgroups G, R2, L2, prefetch, control
  * wave, w-only, non-temporal column loads, register / LDS chunks per
  * workgroup in use, dynamic LDS bytes, resident double2 of the slab, and
  * (gk_res_info only) whether the MGS step launch forms w = A V(:,j) itself,
  * and whether the Arnoldi step's Chebyshev(k) pass forms z = A v in its own
  * stage 0 (1 / 0; -1 on a multi-rank context whose smallest slab is not known
- * until its first solve).
+ * until its first solve), and the threads per workgroup (= double2 per chunk).
  * gk_res_plan_query: pure host computation for a slab of nloc unknowns on a
  * device with `cus` compute units shared by `share` contexts; hh != 0 the
  * reflection chains' plan; nt: -1 auto (from nloc), 0 / 1 forced.  No device
@@ -299,7 +299,7 @@ int gk_sync(gk_ctx *ctx);
 #define GK_RES_PAIRS_LDS 3
 #define GK_RES_WONLY 4
 #define GK_RES_WCOL 5
-#define GK_RES_INFO_LEN 14
+#define GK_RES_INFO_LEN 15
 int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, long long *info);
 int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 

@@ -1,11 +1,11 @@
 # Round 4: evidence of the tree as it stands -- the default bench line (with
 # the reference CPU baseline and the config legs), the Householder and
 # Chebyshev(8) lines, the per-GPU loads of the 2/4/8-GPU splits, rocprofv3
-# kernel stats of the default and 2896^2 runs, config 4 on the resident kernel.
+# kernel stats of the default and 2896^2 runs; the whole GPU suite first.
 OUT=gpurun_out/r04g
 source tools/gpu_lib.sh
 T="python -u -m pytest -v --timeout 200 --timeout-method thread -p no:cacheprovider"
-step t_config4 300 $T tests/test_gpu_configs.py -k "config4"
+step gpu_tests 600 $T tests -m gpu
 step bench_default 500 python -u bench.py
 step bench_hh 300 python -u bench.py --no-cpu --no-configs --method hh
 step bench_cheb 300 python -u bench.py --no-cpu --no-configs --prec cheb
