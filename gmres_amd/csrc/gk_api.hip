@@ -706,34 +706,36 @@ struct ResPlan {
 
 // Column-cache variant (k_mgs_wpc): w of up to RES_PC_RW chunks per thread in
 // registers, the running column of RES_PC_RX of them in registers and of
-// RES_PC_LX in LDS (26 + 38 = all 64: the slab of one GPU of 4096^2 / 2 and of
-// 8192^2 / 8).  A pass streams the one column it reads in batches of WB chunks
-// (8 measured best: 4, 16 and a software-pipelined 8 were slower,
-// profiles/r04/ab_wpc_r04c.jsonl / ab_wpc_r04d.jsonl); the reflection chains
-// keep 6 (8 spills there).  PC_TOUCH > 0 touches the first chunks of the next
-// pass's dot column into L2 during each all-gather: it shortened the pass and
-// lengthened the wait by as much (2896^2: touch 28 / 16 / 0 -> 18.2 / 17.8 /
-// 17.6 us per projection, profiles/r04/ab_wpc_touch_r04e.jsonl), so it is off.
+// RES_PC_LX in LDS; a pass streams its dot column in batches of WB chunks.
+// PC_NT = threads per workgroup.  512 (default, two waves per SIMD: one wave's
+// batch is in flight while the other consumes its own): 32 chunks of w per
+// thread, 4 + 19 of the column cached (the 9 others read V_i too: 10.25 B per
+// unknown at 2896^2), batches of 4; at 2896^2 15.5 us per projection against 17.6
+// for the one-wave build (profiles/r04/ab_pc512_r04j.jsonl) -- 13 + 19 cached spill
+// at 256 VGPRs per wave (the two-wave budget).  256 (one wave per SIMD, the first
+// build): 64 chunks per thread, 26 + 38 cached (8 B per unknown), batches of 8
+// (4, 16 and a software-pipelined 8 were slower, ab_wpc_r04c/d), 6 for the
+// reflection chains.  PC_TOUCH > 0 touches the first chunks of the next pass's dot
+// column into L2 during each all-gather: on the one-wave build it shortened the
+// pass and lengthened the wait by as much (2896^2: touch 28 / 16 / 0 -> 18.2 /
+// 17.8 / 17.6 us per projection, ab_wpc_touch_r04e), so it is off.
+#ifndef GK_RES_PC_NT
+#define GK_RES_PC_NT 512
+#endif
 #ifndef GK_RES_PC_WB
-#define GK_RES_PC_WB 8
+#define GK_RES_PC_WB (GK_RES_PC_NT == 512 ? 4 : 8)
 #endif
 #ifndef GK_RES_PC_WB_HH
-#define GK_RES_PC_WB_HH 6
+#define GK_RES_PC_WB_HH (GK_RES_PC_NT == 512 ? 4 : 6)
 #endif
 #ifndef GK_RES_PC_TOUCH
 #define GK_RES_PC_TOUCH 0
 #endif
-// PC_NT: threads per workgroup -- 512 (two waves per SIMD: one consumes a batch
-// while the other's loads are in flight) holds the same 64 x 256 double2 of w per
-// workgroup as 256 threads x 64 chunks, at 32 chunks per thread.
-#ifndef GK_RES_PC_NT
-#define GK_RES_PC_NT 256
+#ifndef GK_RES_PC_RX
+#define GK_RES_PC_RX (GK_RES_PC_NT == 512 ? 4 : 26)
 #endif
 constexpr int RES_PC_NT = GK_RES_PC_NT;
 static_assert(RES_PC_NT == 256 || RES_PC_NT == 512, "column-cache workgroups of one or two waves per SIMD");
-#ifndef GK_RES_PC_RX
-#define GK_RES_PC_RX (RES_PC_NT == 512 ? 13 : 26)
-#endif
 constexpr int RES_PC_RW = RES_PC_NT == 512 ? 32 : 64, RES_PC_RX = GK_RES_PC_RX, RES_PC_LX = RES_PC_NT == 512 ? 19 : 38;
 constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH, RES_PC_TOUCH = GK_RES_PC_TOUCH;
 
@@ -797,14 +799,16 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         p.l2e = (int)std::min<i64>(lmax, (rest + G - 1) / G);
         p.nres2 = std::min<i64>(nchf, G * (p.r2e + p.l2e)) * dt;
     };
-    // The column-cache variant where it moves at least 1.5x fewer bytes than both
-    // large-slab variants: its one wave per SIMD streams at ~4.7 TB/s where the two
-    // waves of k_mgs_res reach ~6.8 (r04c-e), so the byte saving must pay for that.
-    // 2896^2 (= one GPU of 4096^2 / 2, 8192^2 / 8): 8 vs 14 B/unknown -> 17.6 vs
-    // 18.9 us per projection; 2048^2 (4096^2 / 4): 8 vs 10 -> 11.3-11.5 vs 9.6 us
-    // (profiles/r04/ab_wpc_touch_r04e.jsonl), kept on k_mgs_res.
+    // The column-cache variant where it moves fewer bytes than both large-slab
+    // variants.  The two-wave build streams as fast as k_mgs_res (2896^2: 10.25 vs
+    // 14 B/unknown -> 15.5 vs 18.8 us per projection; 2048^2: 8 vs 10 -> 8.8 vs 9.6,
+    // profiles/r04/ab_pc512_r04j.jsonl).  The one-wave build streamed at ~4.7 TB/s
+    // to k_mgs_res's ~6.8, so there it had to save a third of the bytes (2048^2 was
+    // slower on it: 11.3-11.5 vs 9.6 us, ab_wpc_touch_r04e).
     const bool pc_fits = n2 <= (i64)gmax * RES_PC_RW * RES_PC_NT;
-    const bool pc_pays = pc_fits && 3 * pc_bytes(n2, gmax) <= 2 * std::min(pairs_bytes(n2, gmax), wonly_bytes(n2, gmax));
+    const i64 other_bytes = std::min(pairs_bytes(n2, gmax), wonly_bytes(n2, gmax));
+    const bool pc_pays = pc_fits && (RES_PC_NT == 512 ? pc_bytes(n2, gmax) < other_bytes
+                                                      : 3 * pc_bytes(n2, gmax) <= 2 * other_bytes);
     if (p.r2 >= need || cap < RES_R2_BIG) {
         p.G = gcw;
         p.pf = p.cw = true;

@@ -68,10 +68,10 @@ WCASES = [  # w-only variant (one wave per SIMD): few workgroups so the LDS and 
 ]
 
 
-PCASES = [  # column-cache variant (k_mgs_wpc), forced: cached registers + LDS, streamed rest, odd N
-    (300, 20, "identity", 0, 64),    # 4 workgroups x 44 chunks (26 in registers, 18 in LDS), a streamed tail
-    (181, 16, "cbpr2", 0, 128),      # odd N (tail element), 32 chunks: registers + a few LDS chunks
-    (512, 24, "cheb", 0, 32),        # 8 workgroups x 64 chunks: exactly the 4096^2 / 2 share
+PCASES = [  # column-cache variant (k_mgs_wpc, 512 threads), forced: cached registers + LDS, uncached, streamed
+    (300, 20, "identity", 0, 64),    # 4 workgroups x 22 chunks (4 in registers, 18 in LDS), a streamed tail
+    (181, 16, "cbpr2", 0, 128),      # odd N (tail element), 2 x 16 chunks
+    (512, 24, "cheb", 0, 32),        # 8 workgroups x 32 chunks: exactly the 4096^2 / 2 share (9 uncached)
 ]
 
 
@@ -141,6 +141,7 @@ HCASES = [
 HPCASES = [  # the column-cache variant's reflection chains (forced)
     (300, 20, "identity", 0, 64, 0),
     (181, 16, "cbpr2", 0, 64, 0),
+    (512, 24, "identity", 0, 32, 0),  # the full 32-chunk share: uncached chunks too
 ]
 
 

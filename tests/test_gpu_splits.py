@@ -37,7 +37,7 @@ M = 95
 # grid, expected variant, the production split it stands for
 CASES = [
     (1448, "pairs", "4096^2 on 8 GPUs"),
-    (2048, "pairs+lds", "4096^2 on 4 GPUs"),
+    (2048, "w+column", "4096^2 on 4 GPUs"),
     (2896, "w+column", "4096^2 on 2 GPUs, 8192^2 on 8 GPUs"),
     (4096, "w-only", "4096^2 on 1 GPU (per-workgroup load)"),
 ]

@@ -23,22 +23,22 @@ def _plan(N, R, share=1, hh=False, nt=-1):
 @pytest.mark.parametrize("hh", [False, True])
 @pytest.mark.parametrize("N,R,variant,r2e,l2e,nt", [
     (4096, 1, "w-only", None, 38, 1),      # the bench line (config 1), config 3 and 5
-    (4096, 2, "w+column", 64, 0, 1),       # 8.4 M unknowns per GPU: w in registers, its column cached
-    (4096, 4, "pairs+lds", 12, 4, 0),      # 4.2 M (w+column 8 vs 10 B/unknown: not the 1.5x it needs)
+    (4096, 2, "w+column", 32, 0, 1),       # 8.4 M unknowns per GPU: w in registers, its column cached
+    (4096, 4, "w+column", 16, 0, 1),       # 4.2 M (8 vs 10 B/unknown of k_mgs_res<12,4>)
     (4096, 8, "pairs", 8, 0, 0),           # 2.1 M (w+column ties at 8 B/unknown: the older kernel kept)
-    (8192, 8, "w+column", 64, 0, 1),       # config 4: 8.4 M per GPU
+    (8192, 8, "w+column", 32, 0, 1),       # config 4: 8.4 M per GPU
     (1024, 1, "prefetch", 5, 0, 0),        # config 2
 ])
 def test_production_splits(N, R, variant, r2e, l2e, nt, hh):
     p = _plan(N, R, hh=hh)
     assert p["variant"] == variant and p["G"] == 256
     assert p["l2e"] == l2e and p["nt"] == nt
-    if variant == "w+column":  # 26 register + 38 LDS chunks of the column: all of a 64-chunk share cached
-        assert (p["r2"], p["l2"], p["lds"]) == (26, 38, 38 * 256 * 16)
+    if variant == "w+column":  # 512 threads: 4 register + 19 LDS chunks of the column cached
+        assert (p["r2"], p["l2"], p["lds"], p["wt"]) == (4, 19, 19 * 512 * 16, 512)
     if r2e is not None:
         assert p["r2e"] == r2e
     else:  # w-only: 88 (MGS-R) / 90 (reflection chains) register chunks of 256 double2
-        assert p["r2e"] == (90 if hh else 88)
+        assert p["r2e"] == (90 if hh else 88) and p["wt"] == 256
 
 
 @pytest.mark.parametrize("R", [2, 4, 8])
@@ -52,12 +52,12 @@ def test_ranks_on_one_gpu_carry_the_production_load(N, prod, R):
     assert t["G"] == 256 // R and p["G"] == 256 and t["nt"] == p["nt"]
     for k in ("variant", "r2e", "l2e"):
         assert t[k] == p[k], (k, t, p)
-    dt = 256 if p["variant"] in ("w-only", "w+column") else 512
+    dt = p["wt"]
     # resident double2 per workgroup agree within one chunk (ragged last chunk)
     assert abs(t["nres2"] / t["G"] - p["nres2"] / p["G"]) <= dt
 
 
 def test_query_rejects_bad_arguments():
-    buf = (_native.c_ll * 12)()
+    buf = (_native.c_ll * len(_native.RES_INFO_KEYS))()
     assert _native.hip().gk_res_plan_query(1, 256, 1, 0, -1, buf) == -1
     assert _native.hip().gk_res_plan_query(1 << 20, 0, 1, 0, -1, buf) == -1
