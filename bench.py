@@ -465,7 +465,8 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: d
         roof["ceiling"] = "hbm: every compulsory byte is a DRAM byte (non-temporal column loads / register reuse)"
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf) and on_res and args.method == "mgsr":
-        key, scale = pmc_lookup(json.load(open(tf)), variant, nloc, m, args.prec, args.method)
+        key, scale = pmc_lookup(json.load(open(tf)), variant, nloc, m, args.prec, args.method,
+                                int((plan or {}).get("G", 256)))
         pm = json.load(open(tf)).get(key) if key else None
         if pm and bool(pm.get("sten", False)) != sten:  # measured on the other step flow: not this kernel's bytes
             pm = None
@@ -484,20 +485,25 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: d
     return roof
 
 
-def pmc_lookup(db: dict, variant: str, nloc: int, m: int, prec: str, method: str) -> tuple[str | None, float]:
-    """The PMC entry of this kernel: the exact slab, else the same variant on a
-    slab within 2 % of this one (4096^2 / 2 and 8192^2 / 8 have 8,388,608
-    unknowns per GPU, the single-GPU stand-in 2896^2 has 8,386,816), its bytes
-    scaled by the unknown count."""
+def pmc_lookup(db: dict, variant: str, nloc: int, m: int, prec: str, method: str,
+               G: int = 256) -> tuple[str | None, float]:
+    """The PMC entry of this kernel: the exact slab on the same workgroup count,
+    else the same variant whose per-workgroup load (unknowns / workgroups) is
+    within 2 % of this one -- 4096^2 / 2 and 8192^2 / 8 have 8,388,608 unknowns
+    per GPU, the single-GPU stand-in 2896^2 has 8,386,816; a same-device
+    rehearsal rank holds half of 2896^2 on 128 workgroups -- its bytes scaled by
+    the unknown count.  Entries without "G" were measured on 256 workgroups."""
     key = pmc_key(variant, nloc, m, prec, method)
-    if key in db:
+    if key in db and int(db[key].get("G", 256)) == G:
         return key, 1.0
-    best = None
+    load = nloc / max(1, G)
+    best, bdev = None, None
     for k, v in db.items():
-        if (k.startswith(f"res_{variant}_") and k.endswith(f"_{m}_{prec}_{method}") and v.get("nloc")
-                and abs(v["nloc"] - nloc) <= 0.02 * nloc):
-            if best is None or abs(v["nloc"] - nloc) < abs(db[best]["nloc"] - nloc):
-                best = k
+        if not (k.startswith(f"res_{variant}_") and k.endswith(f"_{m}_{prec}_{method}") and v.get("nloc")):
+            continue
+        dev = abs(v["nloc"] / int(v.get("G", 256)) - load)
+        if dev <= 0.02 * load and (best is None or dev < bdev):
+            best, bdev = k, dev
     return (best, nloc / db[best]["nloc"]) if best else (None, 1.0)
 
 

@@ -254,3 +254,9 @@ def test_pmc_lookup_by_variant_and_slab():
     k, s = bench.pmc_lookup(db, "w+column", 4096 * 4096 // 2, 95, "identity", "mgsr")
     assert k == "res_w+column_8386816_95_identity_mgsr" and s == pytest.approx(8388608 / 8386816)
     assert bench.pmc_lookup(db, "w+column", 4096 * 4096, 95, "identity", "mgsr") == (None, 1.0)
+    # a same-device rehearsal rank: half of 2896^2 on 128 workgroups carries the 2896^2 load per
+    # workgroup (not the 2048^2 slab's, whose unknown count it shares)
+    k, s = bench.pmc_lookup(db, "w+column", 2896 * 2896 // 2, 95, "identity", "mgsr", G=128)
+    assert k == "res_w+column_8386816_95_identity_mgsr" and s == pytest.approx(0.5)
+    k, s = bench.pmc_lookup(db, "w+column", 2048 * 2048, 95, "identity", "mgsr")
+    assert k == "res_w+column_4194304_95_identity_mgsr" and s == 1.0

@@ -60,7 +60,8 @@ def res_fit(a):
     if a.variant and plan["variant"] != a.variant:
         raise SystemExit(f"the plan query selects {plan['variant']}, not {a.variant}")
     model = {int(j): bench.res_launch_bytes(plan, n, 2 * int(j), mgs=True, sten=a.sten) for j in js}
-    entry = {"kernel": a.kernel, "variant": plan["variant"], "nloc": n, "launches_sampled": int(a.probe_m),
+    entry = {"kernel": a.kernel, "variant": plan["variant"], "nloc": n, "G": int(plan["G"]),
+             "launches_sampled": int(a.probe_m),
              "bytes_fixed": float(c),
              "bytes_per_projection": float(b), "bytes_per_unknown_per_projection": float(b) / n,
              "fit_residual_max_rel": float(np.max(np.abs(y - (b * 2 * js + c)) / y)),
