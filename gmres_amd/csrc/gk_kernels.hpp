@@ -1039,6 +1039,11 @@ static_assert(RES_NREP >= 1 && RES_NREP * XS_REP_STEP <= XS_MAXV, "replicas must
 // vs 9.66 and 1024^2 4.12 vs 4.28 -- a poll is cheaper once 32 readers share a copy.
 constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
 constexpr int RES_POLL_SLEEP_SMALL = GK_RES_POLL_SLEEP_SMALL;
+#ifndef GK_RES_POLL_SLEEP_PC
+#define GK_RES_POLL_SLEEP_PC 16
+#endif
+// the column-cache kernel k_mgs_wpc (A/B knob)
+constexpr int RES_POLL_SLEEP_PC = GK_RES_POLL_SLEEP_PC;
 
 // TR: the trace stamps (gk_profile_res_trace) are compiled into the MGS-R launches only
 // (the reflection kernels are at the edge of the register file).
@@ -2191,7 +2196,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_wpc(ResArgs a) {
         if (t == 0) xdone = 0;
         __syncthreads();
         if (t < 64) {
-            res_exchange<NT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
+            res_exchange<NT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP_PC>(a, xi, sm, bc, &okf);
             if (t == 0) *(volatile int *)&xdone = 1;
         } else if constexpr (TCHP > 0) {
             if (touch_col >= 0) {
