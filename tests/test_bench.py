@@ -260,3 +260,23 @@ def test_pmc_lookup_by_variant_and_slab():
     assert k == "res_w+column_8386816_95_identity_mgsr" and s == pytest.approx(0.5)
     k, s = bench.pmc_lookup(db, "w+column", 2048 * 2048, 95, "identity", "mgsr")
     assert k == "res_w+column_4194304_95_identity_mgsr" and s == 1.0
+
+
+def test_read_scale_finds_bench_lines_in_a_driver_file():
+    """tools/read_scale.py: bench lines nested anywhere in the driver's scaling
+    file (dicts, lists, stdout tails) are set beside the committed prediction."""
+    import json
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import read_scale
+
+    line = {"metric": "m", "value": 500.0, "n_gpus": 2, "config": {"resident_variant": "w+column"},
+            "diagnostics": {"resident_split_per_unit_us": {"mgs_step": {"wait_us": 5.0}}}}
+    doc = {"runs": [{"n": 2, "run": {"stdout_tail": "log\n" + json.dumps(line) + "\n"}}, {"n": 4, "skipped": True}]}
+    lines = read_scale.bench_lines(doc)
+    assert lines == [line]
+    pred = {"points": [{"world": 2, "grid": 4096, "predicted_it_s": [450.0, 600.0],
+                        "predicted_wait_per_projection_us": [4.0, 7.0]}]}
+    (row,) = read_scale.compare(lines, pred)
+    assert row["verdict"] == "inside band" and row["wait_us"] == 5.0 and row["variant"] == "w+column"
