@@ -699,6 +699,7 @@ struct ResPlan {
     int r2e = 0, l2e = 0;  // chunks per workgroup used: the resident prefix spread evenly over G
     bool pf = false, nt = false, cw = false, wo = false;
     bool pc = false;       // column-cache variant (k_mgs_wpc): w in registers, running column cached
+    bool pcs = false;      // ... its 16-chunk instantiation (whole column in registers)
     int wt = 0;            // threads per workgroup = double2 per chunk (set by plan_resident)
     i64 nres2 = 0;
     int lds = 0;
@@ -738,6 +739,13 @@ constexpr int RES_PC_NT = GK_RES_PC_NT;
 static_assert(RES_PC_NT == 256 || RES_PC_NT == 512, "column-cache workgroups of one or two waves per SIMD");
 constexpr int RES_PC_RW = RES_PC_NT == 512 ? 32 : 64, RES_PC_RX = GK_RES_PC_RX, RES_PC_LX = RES_PC_NT == 512 ? 19 : 38;
 constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH, RES_PC_TOUCH = GK_RES_PC_TOUCH;
+// Slabs of at most 16 chunks per thread (two-wave build): k_mgs_wpc<16, 16, 0> -- w and
+// its whole column in registers, no LDS, half the unrolled pass of the 32-chunk kernel.
+#ifndef GK_RES_PC_SMALL
+#define GK_RES_PC_SMALL 1
+#endif
+constexpr bool RES_PCS = GK_RES_PC_SMALL != 0 && RES_PC_NT == 512;
+constexpr int RES_PCS_RW = 16, RES_PCS_RX = 16, RES_PCS_LX = 0;
 
 // Modelled bytes per projection of a slab of n2 double2 on G workgroups (the
 // unit of pairs_bytes / wonly_bytes: 8 per double2 whose w and running column are
@@ -745,6 +753,7 @@ constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH, RES_PC_T
 // column-cache variant: the cached pairs, the rest of the register-held w, the
 // streamed rest.
 i64 pc_bytes(i64 n2, int G) {
+    if (RES_PCS && n2 <= (i64)G * RES_PCS_RW * RES_PC_NT) return 8 * n2;  // the 16-chunk kernel: all cached
     const i64 cap = (i64)G * RES_PC_RW * RES_PC_NT, cached = (i64)G * (RES_PC_RX + RES_PC_LX) * RES_PC_NT;
     const i64 r = std::min(n2, cap), c = std::min(r, cached);
     return 8 * c + 16 * (r - c) + 32 * (n2 - r);
@@ -817,11 +826,12 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         // w wholly in registers, the running column cached (k_mgs_wpc): 8 B/unknown
         p.G = gmax;
         p.pc = true;
-        p.r2 = RES_PC_RX;
-        p.l2 = RES_PC_LX;
         p.wt = RES_PC_NT;
         spread(RES_PC_NT, RES_PC_RW, 0);
-        p.lds = RES_PC_LX * RES_PC_NT * (int)sizeof(double2);
+        p.pcs = RES_PCS && p.r2e <= RES_PCS_RW;
+        p.r2 = p.pcs ? RES_PCS_RX : RES_PC_RX;
+        p.l2 = p.pcs ? RES_PCS_LX : RES_PC_LX;
+        p.lds = p.l2 * RES_PC_NT * (int)sizeof(double2);
         p.nt = true;
         return;
     } else if (tune_wonly > 0 || (tune_wonly < 0 && wonly_pays(n2, gmax))) {
@@ -942,22 +952,31 @@ int launch_wres(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     }
 }
 
-template <int MODE>
-int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+template <int RW, int RX, int LX, int MODE>
+int launch_wpc_k(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     constexpr int WBT = MODE == gk::RES_MGS ? RES_PC_WB : RES_PC_WB_HH;
     static std::atomic<int> attr[ATTR_DEVS];
     if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
-    if (attr[c->dev].load() < p.lds) {
+    if (p.r2e > RW || p.lds < LX * RES_PC_NT * (int)sizeof(double2))
+        return set_err(GK_ERR_STATE, "column-cache plan (%d chunks, %d B LDS) does not fit k_mgs_wpc<%d,%d,%d>", p.r2e,
+                       p.lds, RW, RX, LX);
+    if (p.lds > 0 && attr[c->dev].load() < p.lds) {
         HIPCHK(hipFuncSetAttribute(
-            reinterpret_cast<const void *>(
-                &gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT, RES_PC_TOUCH, RES_PC_NT>),
+            reinterpret_cast<const void *>(&gk::k_mgs_wpc<RW, RX, LX, MODE, WBT, RES_PC_TOUCH, RES_PC_NT>),
             hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
         attr[c->dev] = p.lds;
     }
-    gk::k_mgs_wpc<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE, WBT, RES_PC_TOUCH, RES_PC_NT>
-        <<<p.G, RES_PC_NT, p.lds, c->st>>>(a);
+    gk::k_mgs_wpc<RW, RX, LX, MODE, WBT, RES_PC_TOUCH, RES_PC_NT><<<p.G, RES_PC_NT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
+}
+
+template <int MODE>
+int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    if constexpr (RES_PCS) {
+        if (p.pcs) return launch_wpc_k<RES_PCS_RW, RES_PCS_RX, RES_PCS_LX, MODE>(c, p, a);
+    }
+    return launch_wpc_k<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE>(c, p, a);
 }
 
 int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {

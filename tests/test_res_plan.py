@@ -33,8 +33,10 @@ def test_production_splits(N, R, variant, r2e, l2e, nt, hh):
     p = _plan(N, R, hh=hh)
     assert p["variant"] == variant and p["G"] == 256
     assert p["l2e"] == l2e and p["nt"] == nt
-    if variant == "w+column":  # 512 threads: 4 register + 19 LDS chunks of the column cached
-        assert (p["r2"], p["l2"], p["lds"], p["wt"]) == (4, 19, 19 * 512 * 16, 512)
+    if variant == "w+column":  # 512 threads: 4 register + 19 LDS chunks of the column cached;
+        # slabs of <= 16 chunks per thread: the 16-chunk kernel, the whole column in registers
+        want = (16, 0, 0) if r2e <= 16 else (4, 19, 19 * 512 * 16)
+        assert (p["r2"], p["l2"], p["lds"], p["wt"]) == want + (512,)
     if r2e is not None:
         assert p["r2e"] == r2e
     else:  # w-only: 88 (MGS-R) / 90 (reflection chains) register chunks of 256 double2
