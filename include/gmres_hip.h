@@ -279,7 +279,9 @@ int gk_sync(gk_ctx *ctx);
  *   GK_RES_WCOL       k_mgs_wpc: w in registers and the running Krylov column cached
  *                     (registers + LDS) -- 8 B per unknown per projection for slabs of
  *                     up to 64 x 256 double2 per workgroup (one GPU of 4096^2 / 2 and
- *                     of 8192^2 / 8), in 512-thread workgroups (two waves per SIMD).
+ *                     of 8192^2 / 8), in 512-thread workgroups (two waves per SIMD); slabs
+ *                     of <= 16 chunks per thread (4096^2 / 4) keep the whole column in
+ *                     registers (r2 = 16, l2 = 0).
  * info[GK_RES_INFO_LEN]: variant, workgroups G, R2, L2, prefetch, control
  * wave, w-only, non-temporal column loads, register / LDS chunks per
  * workgroup in use, dynamic LDS bytes, resident double2 of the slab, and
