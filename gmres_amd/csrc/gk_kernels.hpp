@@ -1038,6 +1038,13 @@ static_assert(RES_NREP >= 1 && RES_NREP * XS_REP_STEP <= XS_MAXV, "replicas must
 // (profiles/r02/ab_rep_*.jsonl) 4 instead of 16: 4096^2 41.8 vs 41.5 us, but 2048^2 9.57
 // vs 9.66 and 1024^2 4.12 vs 4.28 -- a poll is cheaper once 32 readers share a copy.
 constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
+#ifndef GK_RES_PUSHER_FAST
+#define GK_RES_PUSHER_FAST 1
+#endif
+// N ranks: workgroup 0, which pushes the rank total to the peers once its sweep
+// completes, polls its granules without the sleep (its detection delay is on
+// every rank's critical path; the other workgroups' is not).
+constexpr bool RES_PUSHER_FAST = GK_RES_PUSHER_FAST != 0;
 constexpr int RES_POLL_SLEEP_SMALL = GK_RES_POLL_SLEEP_SMALL;
 #ifndef GK_RES_POLL_SLEEP_PC
 #define GK_RES_POLL_SLEEP_PC 16
@@ -1192,7 +1199,10 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
                     if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(SLEEP);
+                if (RES_PUSHER_FAST && a.nranks > 1 && blockIdx.x == 0)
+                    __builtin_amdgcn_s_sleep(1);  // the rank-total pusher: push as soon as the sweep completes
+                else
+                    __builtin_amdgcn_s_sleep(SLEEP);
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {  // workgroups in increasing order per lane pair
