@@ -270,6 +270,21 @@ def cpu_baseline(N: int, m: int, prec: str, degree: int, method: str, cap_full: 
 
 # ------------------------------------------------------------- launcher -----
 def _free_port() -> int:
+    """A port for the self-launched rendezvous, below the kernel's ephemeral range
+    (32768-60999 by default): an ephemeral port that probed free can be taken by
+    a client connection (or sit in TIME_WAIT after the previous run's ranks) by
+    the time torch.distributed.run's store binds it (EADDRINUSE, seen r04t)."""
+    import random
+
+    rng = random.Random(os.getpid() ^ int(time.time() * 1e6))
+    for _ in range(200):
+        port = rng.randrange(20000, 32000)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]

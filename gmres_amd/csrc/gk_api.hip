@@ -160,6 +160,7 @@ struct gk_ctx {
     int tune_graph = 1;       // launch-path MGS-R steps captured as hipGraphs (RCCL / no collective)
     int tune_res_qdef = -1;   // k_mgs_res NT: V_q of the LDS / streamed parts with the default policy (-1 auto)
     int tune_res_pc = -1;     // column-cache variant k_mgs_wpc: -1 by the byte model, 0 never, 1 where it fits
+    int tune_res_fold = 1;    // N ranks, device exchange: the first dot's rank hop inside the MGS step launch
     std::vector<hipGraphExec_t> gstep;  // captured step j (launch path), valid for partial-slab count gkey
     std::vector<unsigned> gxs;          // device exchanges in captured step j (their sequence numbers)
     int gkey = -1;
@@ -1010,13 +1011,15 @@ int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 //    its unit input e_{unit_g} itself.
 //  sten_v (RES_MGS, w-only variant): the launch forms w = A sten_v itself and the
 //    first dot with it (no pin); the halo lines of sten_v must be in c->hlo / c->hhi.
-enum { RESF_CLOSE_HH = 1, RESF_UNIT_INIT = 2 };
+enum { RESF_CLOSE_HH = 1, RESF_UNIT_INIT = 2, RESF_PIN_LOCAL = 4 };
 int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, double *hs, double *hcopy,
              int mode = gk::RES_MGS, double *w = nullptr, i64 unit_g = -1, int flags = 0,
              const double *sten_v = nullptr) {
     ProfScope ps(c, GK_KID_RES);
     const bool close = (flags & RESF_CLOSE_HH) && mode == gk::RES_HH_UP;
-    if (flags != 0 && !p.wo) return set_err(GK_ERR_STATE, "resident flags %d need the w-only variant", flags);
+    if ((flags & ~RESF_PIN_LOCAL) != 0 && !p.wo)
+        return set_err(GK_ERR_STATE, "resident flags %d need the w-only variant", flags);
+    const bool pin_local = (flags & RESF_PIN_LOCAL) && mode == gk::RES_MGS && c->xs_on && c->nranks > 1;
     if (sten_v != nullptr && (!p.wo || mode != gk::RES_MGS || c->N % 2 != 0))
         return set_err(GK_ERR_STATE, "the stencil prologue needs the w-only MGS step and even N");
     // exchanges of the launch (the stencil prologue adds the first dot's)
@@ -1073,8 +1076,9 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
         a.peers = c->xs_peers;
         a.nranks = c->nranks;
         a.rank = c->rank;
-        a.xseq0 = c->xs_seq;
-        c->xs_seq += (unsigned)np;
+        a.pin_local = pin_local ? 1 : 0;  // the first dot's rank hop takes the launch's first number
+        a.xseq0 = c->xs_seq + (pin_local ? 1u : 0u);
+        c->xs_seq += (unsigned)np + (pin_local ? 1u : 0u);
     }
     return launch_res(c, p, a);
 }
@@ -2116,8 +2120,12 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
     CHK(op_precond(c, V + (i64)(j - 1) * ld, c->w, false, gk::ACC_DOT, V, slot(c, s0)));
     int np = c->last_np;
     if (res) {  // the whole cascade + norm + scale as one resident launch
-        CHK(allreduce(c, slot(c, s0), np));
-        CHK(res_step(c, j, rp, slot(c, s0), np, hs, c->hallh_dev + (i64)(j - 1) * m2));
+        // N ranks on the device exchange: the first dot's rank totals inside the launch
+        // (GK_TUNE_RES_FOLD) instead of a k_xchg launch before it
+        const bool fold = c->tune_res_fold && c->xs_on && c->nranks > 1;
+        if (!fold) CHK(allreduce(c, slot(c, s0), np));
+        CHK(res_step(c, j, rp, slot(c, s0), np, hs, c->hallh_dev + (i64)(j - 1) * m2, gk::RES_MGS, nullptr, -1,
+                     fold ? RESF_PIN_LOCAL : 0));
         HIPCHK(hipEventRecord(c->ev_step[j], c->st));
         c->prof_on_step = true;
         return GK_OK;
@@ -2484,6 +2492,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_GRAPH: c->tune_graph = value != 0; break;
         case GK_TUNE_RES_QDEF: c->tune_res_qdef = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_RES_PC: c->tune_res_pc = value < 0 ? -1 : (value != 0); break;
+        case GK_TUNE_RES_FOLD: c->tune_res_fold = value != 0; break;
         case GK_TUNE_VERR_ORDER: c->tune_verr_order = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");

@@ -906,6 +906,7 @@ struct ResArgs {
     // with the default policy (it is the next pass's AXPY column V_i: then an
     // Infinity-Cache hit), V_i non-temporal -- the w-only kernel's policy
     int qdef;
+    int pin_local;        // N ranks, MGS: pin is this rank's partial slab only (res_pin_fold)
 };
 constexpr int RES_TRACE_X = 2 * RHMAX + 2;  // exchanges recorded per workgroup (all of one launch)
 
@@ -1051,6 +1052,62 @@ constexpr int RES_POLL_SLEEP_SMALL = GK_RES_POLL_SLEEP_SMALL;
 #endif
 // the column-cache kernel k_mgs_wpc (A/B knob)
 constexpr int RES_POLL_SLEEP_PC = GK_RES_POLL_SLEEP_PC;
+
+// Wave 0 of every workgroup, N ranks: the rank totals of exchange index p
+// (sequence number a.xseq0 + 1 + p).
+__device__ __forceinline__ double res_rank_sum(const ResArgs &a, int p, double acc, bool &all_ok) {
+    const int lane = threadIdx.x;
+    // Rank totals: workgroup 0 pushes this rank's total into every peer's region,
+    // once per replica (value slot XS_REP_STEP * r of its source row: a line of its
+    // own), and every workgroup reads replica blockIdx % NREP -- 1/NREP of the grid
+    // polls each line instead of all of it.  A slot is rewritten two exchanges later
+    // at the earliest, after every workgroup of every rank has read it (rendezvous).
+    const unsigned seq = a.xseq0 + 1u + (unsigned)p, par = seq & 1u;
+    if (blockIdx.x == 0) {
+        const u64 bits = (u64)__double_as_longlong(acc);
+        for (int k = lane; k < 2 * RES_NREP * a.nranks; k += 64) {
+            const int dst = k / (2 * RES_NREP), r = (k >> 1) % RES_NREP, half = k & 1;
+            xs_put(a.peers.p[dst] + (((i64)par * XS_MAXR + a.rank) * XS_MAXV + XS_REP_STEP * r) * 2 + half, seq,
+                   half ? (unsigned)(bits >> 32) : (unsigned)bits);
+        }
+    }
+    unsigned d = 0;
+    bool ok2 = true;
+    if (lane < 2 * a.nranks) {
+        const int src = lane >> 1, half = lane & 1, r = (int)(blockIdx.x % RES_NREP);
+        const int g = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV + XS_REP_STEP * r) * 2 + half,
+                             seq, wall_clock64() + a.timeout, &d, a.err);
+        ok2 = g == XG_OK;
+        if (g == XG_LATE) xs_fail(a.err, XSE_RES_RANK, src);
+    }
+    all_ok = all_ok && __all(ok2);
+    double r = 0.0;
+    for (int q = 0; q < a.nranks; ++q) {  // rank order, as k_xchg<XS_SLAB>
+        const unsigned lo = __shfl(d, 2 * q, 64), hi = __shfl(d, 2 * q + 1, 64);
+        const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
+        r = (q == 0) ? v : r + v;
+    }
+    return r;
+}
+
+// pin_local (N ranks, the MGS step): the stencil's first-dot partial slab `pin`
+// is this rank's alone -- no k_xchg launch before the step -- and its total h
+// goes through the rank-total hop here (exchange index -1, the launch's first
+// sequence number), summed in rank order like every in-launch total.
+__device__ __forceinline__ bool res_pin_fold(const ResArgs &a, double &h, double *bc, int *okf) {
+    if (!a.pin_local) return true;
+    if (threadIdx.x < 64) {
+        bool ok = true;
+        const double r = res_rank_sum(a, -1, h, ok);
+        if (threadIdx.x == 0) {
+            bc[0] = r;
+            *okf = ok ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    h = bc[0];
+    return *okf != 0;
+}
 
 // TR: the trace stamps (gk_profile_res_trace) are compiled into the MGS-R launches only
 // (the reflection kernels are at the edge of the register file).
@@ -1214,39 +1271,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
         }
         acc = wave_sum(acc);  // butterfly: the same value on every lane of every workgroup
     }
-    if (all_ok && a.nranks > 1) {
-        // Rank totals: workgroup 0 pushes this rank's total into every peer's region,
-        // once per replica (value slot XS_REP_STEP * r of its source row: a line of its
-        // own), and every workgroup reads replica blockIdx % NREP -- 1/NREP of the grid
-        // polls each line instead of all of it.  A slot is rewritten two exchanges later
-        // at the earliest, after every workgroup of every rank has read it (rendezvous).
-        const unsigned seq = a.xseq0 + 1u + (unsigned)p, par = seq & 1u;
-        if (blockIdx.x == 0) {
-            const u64 bits = (u64)__double_as_longlong(acc);
-            for (int k = lane; k < 2 * RES_NREP * a.nranks; k += 64) {
-                const int dst = k / (2 * RES_NREP), r = (k >> 1) % RES_NREP, half = k & 1;
-                xs_put(a.peers.p[dst] + (((i64)par * XS_MAXR + a.rank) * XS_MAXV + XS_REP_STEP * r) * 2 + half, seq,
-                       half ? (unsigned)(bits >> 32) : (unsigned)bits);
-            }
-        }
-        unsigned d = 0;
-        bool ok2 = true;
-        if (lane < 2 * a.nranks) {
-            const int src = lane >> 1, half = lane & 1, r = (int)(blockIdx.x % RES_NREP);
-            const int g = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV + XS_REP_STEP * r) * 2 + half,
-                                 seq, wall_clock64() + a.timeout, &d, a.err);
-            ok2 = g == XG_OK;
-            if (g == XG_LATE) xs_fail(a.err, XSE_RES_RANK, src);
-        }
-        all_ok = __all(ok2);
-        double r = 0.0;
-        for (int q = 0; q < a.nranks; ++q) {  // rank order, as k_xchg<XS_SLAB>
-            const unsigned lo = __shfl(d, 2 * q, 64), hi = __shfl(d, 2 * q + 1, 64);
-            const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
-            r = (q == 0) ? v : r + v;
-        }
-        acc = r;
-    }
+    if (all_ok && a.nranks > 1) acc = res_rank_sum(a, p, acc, all_ok);
     if (lane == 0) {
         bc[0] = acc;
         *okf = all_ok ? 1 : 0;
@@ -1351,6 +1376,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         double s = 0.0;
         for (int k = t; k < a.npin; k += RT) s += a.pin[k];
         h = block_sum_rt(s, sm);
+        ok = res_pin_fold(a, h, bc, &okf);
     }
     // Projection p: i = p mod j, AXPY w -= h V_i (h = the dot of p), then the
     // dot of projection p+1 with V_q, q = (p+1) mod j -- or ||w||^2 after the
@@ -1932,6 +1958,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 #pragma unroll
         for (int w = 1; w < WT / 64; ++w) h += sm[w];
         __syncthreads();
+        ok = res_pin_fold(a, h, bc, &okf);
     }
     for (int p = 0; p < np && ok; ++p) {
         const int i = res_col(mode, j, p);
@@ -2251,6 +2278,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_wpc(ResArgs a) {
 #pragma unroll
         for (int w = 1; w < NT / 64; ++w) h += sm[w];
         __syncthreads();
+        ok = res_pin_fold(a, h, bc, &okf);
     }
     for (int p = 0; p < np && ok; ++p) {
         const int i = res_col(mode, j, p);

@@ -150,6 +150,64 @@ def test_split_variant_in_process(N, variant, prod, R, method):
         g.close()
 
 
+@pytest.mark.parametrize("N,variant", [(1448, "pairs"), (2048, "w+column"), (2896, "w+column")])
+def test_first_dot_fold(N, variant):
+    """GK_TUNE_RES_FOLD: on 2 ranks the MGS step's first dot <w, V(:,1)> is summed
+    across ranks inside the resident launch (each rank's partial slab summed
+    locally, then the rank-total hop) instead of by a k_xchg launch before it --
+    one collective launch fewer per Arnoldi step, the same cycle up to the
+    summation order of that one dot."""
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+
+    R, nt = 2, _prod_nt(N)
+    parts = ga.slab_partition(N, R)
+    runs = {}
+    for fold in (0, 1):
+        g = ga.LocalGroup(R)
+        ctxs = [ga.Context(N, M, device=0, line0=l0, nlines=nl) for l0, nl in parts]
+        out, err = [None] * R, []
+        try:
+            for r, c in enumerate(ctxs):
+                c.comm_init_local(g, r, max(nl for _, nl in parts))
+            for c in ctxs:
+                c.xchg_local()
+                _tune_forced(c, nt, R)
+                c.tune(nat.GK_TUNE_RES_FOLD, fold)
+            assert all(c.res_info()["variant"] == variant for c in ctxs)
+
+            def work(r):
+                try:
+                    c = ctxs[r]
+                    c.set_rhs_ones()
+                    c.profile(True)
+                    c.profile_reset()
+                    out[r] = (_solve(c, "mgsr"), c.profile_read())
+                except Exception as e:  # pragma: no cover - reported below
+                    err.append(e)
+
+            th = [threading.Thread(target=work, args=(r,)) for r in range(R)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(timeout=110)
+            assert not err, err
+            assert all(o is not None for o in out)
+            runs[fold] = out
+        finally:
+            for c in ctxs:
+                c.close()
+            g.close()
+    (r0, p0), (r1, p1) = runs[0][0], runs[1][0]
+    assert all(np.array_equal(r1.hist_res, o[0].hist_res) for o in runs[1])  # every rank the same decisions
+    assert r1.n_out == r0.n_out == M
+    assert r1.hist_res[0] == pytest.approx(r0.hist_res[0], rel=1e-12)
+    assert np.allclose(r1.final_err[:M], r0.final_err[:M], rtol=1e-9, atol=0)
+    # one all-reduce launch fewer per Arnoldi step
+    assert p0["comm"][1] - p1["comm"][1] == M, (p0["comm"], p1["comm"])
+    assert p1["res"][1] == p0["res"][1] >= M
+
+
 # ------------------------------------------------ two processes (IPC) ------
 
 def _ipc_worker(rank, R, N, nt, method, hq, hin, outq, done):
