@@ -9,13 +9,14 @@ CUs, exactly as a single-GPU run of a grid with the same unknown count does
 (1448^2 ~ 4096^2/8, 2048^2 ~ 4096^2/4, 2896^2 ~ 4096^2/2 and 8192^2/8).  So the
 per-GPU cycle time is that single-GPU cycle (bench.py --grid G, ms_per_step)
 plus what only N ranks pay:
-  * per Arnoldi step, two collective launches on the step's critical path: the
-    halo lines before the stencil (k_xhalo) and the all-reduce of the stencil's
-    fused first dot (k_xchg) -- priced at gk_comm_latency's per-call times;
-  * per projection, the hop of the rank totals inside the resident launch
-    (workgroup 0 of every rank stores its total into every peer's region over
-    xGMI, every workgroup polls its own region): delta_hop.
-  t_cycle(N) = t_cycle_1GPU(n/N) + m (t_halo + t_allreduce) + m (m + 1) delta_hop
+  * per Arnoldi step, one collective launch on the step's critical path: the
+    halo lines before the stencil (k_xhalo), priced at gk_comm_latency's
+    per-call time (the stencil's first dot is summed across ranks inside the
+    resident launch, GK_TUNE_RES_FOLD: one more in-launch hop per step);
+  * per projection (and per step for the first dot), the hop of the rank totals
+    inside the resident launch (workgroup 0 of every rank stores its total into
+    every peer's region over xGMI, every workgroup polls its own region): delta_hop.
+  t_cycle(N) = t_cycle_1GPU(n/N) + m t_halo + m (m + 2) delta_hop
   it/s(N)    = m / t_cycle(N),  value of the N-GPU bench line (max over ranks).
 Bands.  The collective per-call time at the high end is gk_comm_latency of the
 same-device rehearsal (N processes on ONE GPU through IPC, back-to-back calls:
@@ -69,15 +70,15 @@ def predict(hop_lo: float, hop_hi: float, coll_lo: float = 5.0) -> dict:
     for label, world, grid, g1, rel in POINTS:
         cw = comm.get(str(world)) or comm.get(str(max([int(k) for k in comm if k.isdigit()] or [0]))) or {}
         t_ar, t_halo = float(cw.get("allreduce", 10.0)), float(cw.get("halo", 10.0))
-        fixed_lo = 0.0 if world == 1 else M * 2 * coll_lo * 1e-6
+        fixed_lo = 0.0 if world == 1 else M * coll_lo * 1e-6
         b = load(rel)
         if b is None:
             rows.append({"point": label, "missing": rel})
             continue
         t1 = float(b["ms_per_step"]) * 1e-3  # one cycle of the equal-load single-GPU run
         split = ((b.get("diagnostics") or {}).get("resident_split_per_unit_us") or {}).get("mgs_step") or {}
-        extra_fixed = 0.0 if world == 1 else M * (t_ar + t_halo) * 1e-6
-        nproj = M * (M + 1)
+        extra_fixed = 0.0 if world == 1 else M * t_halo * 1e-6
+        nproj = M * (M + 2)  # the 2j projections of every step plus its first dot
         lo = t1 + fixed_lo + (0.0 if world == 1 else nproj * hop_lo * 1e-6)
         hi = t1 + extra_fixed + (0.0 if world == 1 else nproj * hop_hi * 1e-6)
         rows.append({
@@ -100,7 +101,7 @@ def predict(hop_lo: float, hop_hi: float, coll_lo: float = 5.0) -> dict:
     for r in rows:
         if base and "predicted_it_s" in r and r["grid"] == 4096:
             r["predicted_speedup"] = [round(v / base["predicted_it_s"][1], 2) for v in r["predicted_it_s"]]
-    return {"model": "t_cycle(N) = t_cycle_1GPU(n/N) + m (t_halo + t_allreduce) + m (m+1) delta_hop",
+    return {"model": "t_cycle(N) = t_cycle_1GPU(n/N) + m t_halo + m (m+2) delta_hop (first dot folded into the launch)",
             "m": M, "collective_per_call_low_us": coll_lo, "collective_source": f"profiles/{COMM}" if comm else "default 10 us (no rehearsal file)",
             "delta_hop_us": [hop_lo, hop_hi], "points": rows}
 
