@@ -1019,7 +1019,7 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
     const bool close = (flags & RESF_CLOSE_HH) && mode == gk::RES_HH_UP;
     if ((flags & ~RESF_PIN_LOCAL) != 0 && !p.wo)
         return set_err(GK_ERR_STATE, "resident flags %d need the w-only variant", flags);
-    const bool pin_local = (flags & RESF_PIN_LOCAL) && mode == gk::RES_MGS && c->xs_on && c->nranks > 1;
+    const bool pin_local = (flags & RESF_PIN_LOCAL) && mode != gk::RES_HH_DOWN && c->xs_on && c->nranks > 1;
     if (sten_v != nullptr && (!p.wo || mode != gk::RES_MGS || c->N % 2 != 0))
         return set_err(GK_ERR_STATE, "the stencil prologue needs the w-only MGS step and even N");
     // exchanges of the launch (the stencil prologue adds the first dot's)
@@ -2311,9 +2311,12 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
         CHK(stencil(c, gk::OP_PLAIN, gk::ACC_DOT, a));
     }
     int np = c->last_np;
+    // N ranks on the device exchange: <w, P_1> summed across ranks inside the launch (GK_TUNE_RES_FOLD)
+    const bool fold = res && c->tune_res_fold && c->xs_on && c->nranks > 1;
     if (fuse) {  // w = P_j .. P_1 w, ||w(j+1:n)||^2, the fix-up and P(:,j+1), one launch
-        CHK(allreduce(c, slot(c, s0), np));
-        CHK(res_step(c, j, rp, slot(c, s0), np, slot(c, s1), nullptr, gk::RES_HH_UP, c->w, -1, RESF_CLOSE_HH));
+        if (!fold) CHK(allreduce(c, slot(c, s0), np));
+        CHK(res_step(c, j, rp, slot(c, s0), np, slot(c, s1), nullptr, gk::RES_HH_UP, c->w, -1,
+                     RESF_CLOSE_HH | (fold ? RESF_PIN_LOCAL : 0)));
         // H(1:j+1, j) from hb (written by the owner rank's launch) on every rank
         CHK(bcast(c, c->hb, j + 1, owner_of(c, j)));
         {
@@ -2327,8 +2330,9 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
         return GK_OK;
     }
     if (res) {  // w = P_j .. P_1 w and ||w(j+1:n)||^2 as one resident launch
-        CHK(allreduce(c, slot(c, s0), np));
-        CHK(res_step(c, j, rp, slot(c, s0), np, slot(c, s1), nullptr, gk::RES_HH_UP, c->w));
+        if (!fold) CHK(allreduce(c, slot(c, s0), np));
+        CHK(res_step(c, j, rp, slot(c, s0), np, slot(c, s1), nullptr, gk::RES_HH_UP, c->w, -1,
+                     fold ? RESF_PIN_LOCAL : 0));
         std::swap(s0, s1);
         np = 1;  // slot s0[0]: the rank-summed total
     } else {

@@ -367,8 +367,9 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          Infinity-Cache hit (the w-only kernel's policy); 0 = both
  *                          non-temporal; -1 (default) = the measured choice
  *   GK_TUNE_RES_FOLD       1 (default): N ranks on the device exchange -- the MGS step's first dot
- *                          <w, V(:,1)> is summed across ranks inside the resident launch (its
- *                          rank-total hop) instead of by a k_xchg launch before it; 0: the launch
+ *                          <w, V(:,1)> (Householder: <w, P_1>) is summed across ranks inside the
+ *                          resident launch (its rank-total hop) instead of by a k_xchg launch
+ *                          before it; 0: the launch
  *   GK_TUNE_RES_PC         column-cache variant (GK_RES_WCOL): -1 (default) where its modelled
  *                          bytes per projection are at most 2/3 of the pairs and w-only
  *                          variants' (its one-wave pass streams slower); 0 never; 1 wherever
