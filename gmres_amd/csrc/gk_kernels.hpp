@@ -1046,6 +1046,12 @@ constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
 // completes, polls its granules without the sleep (its detection delay is on
 // every rank's critical path; the other workgroups' is not).
 constexpr bool RES_PUSHER_FAST = GK_RES_PUSHER_FAST != 0;
+#ifndef GK_RES_SWEEP_ALL
+#define GK_RES_SWEEP_ALL 0
+#endif
+// N ranks: 1 = every workgroup sweeps the local granules (the earlier protocol),
+// 0 = only workgroup 0 does (A/B knob).  The totals are the same bits either way.
+constexpr bool RES_SWEEP_ALL = GK_RES_SWEEP_ALL != 0;
 constexpr int RES_POLL_SLEEP_SMALL = GK_RES_POLL_SLEEP_SMALL;
 #ifndef GK_RES_POLL_SLEEP_PC
 #define GK_RES_POLL_SLEEP_PC 16
@@ -1218,7 +1224,10 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
             r = (q == 0) ? v : r + v;
         }
         acc = all_ok ? r : 0.0;
-    } else {
+    } else if (RES_SWEEP_ALL || a.nranks == 1 || blockIdx.x == 0) {
+        // (N ranks: only workgroup 0, the pusher, needs this rank's total -- every
+        // workgroup then reads the R rank totals, its own rank's included, so the
+        // others skip the sweep and its polls stay off the stragglers' memory path.)
         // Lane L holds granule L + 64k of each 512-granule sweep: the lo (even L)
         // or hi (odd L) half of workgroup c0/2 + L/2 + 32k.
         for (int c0 = 0; c0 < 2 * G && all_ok; c0 += 512) {
