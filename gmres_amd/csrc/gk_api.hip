@@ -738,7 +738,13 @@ struct ResPlan {
 #endif
 constexpr int RES_PC_NT = GK_RES_PC_NT;
 static_assert(RES_PC_NT == 256 || RES_PC_NT == 512, "column-cache workgroups of one or two waves per SIMD");
+#ifndef GK_RES_PC_RX_MGS
+#define GK_RES_PC_RX_MGS (GK_RES_PC_NT == 512 ? 6 : GK_RES_PC_RX)
+#endif
+// RX_MGS: the MGS step's register-cached chunks (6 fit its register budget; the
+// reflection chains spill 20 B per lane at 6 and keep RX = 4)
 constexpr int RES_PC_RW = RES_PC_NT == 512 ? 32 : 64, RES_PC_RX = GK_RES_PC_RX, RES_PC_LX = RES_PC_NT == 512 ? 19 : 38;
+constexpr int RES_PC_RX_MGS = GK_RES_PC_RX_MGS;
 constexpr int RES_PC_WB = GK_RES_PC_WB, RES_PC_WB_HH = GK_RES_PC_WB_HH, RES_PC_TOUCH = GK_RES_PC_TOUCH;
 // Slabs of at most 16 chunks per thread (two-wave build): k_mgs_wpc<16, 16, 0> -- w and
 // its whole column in registers, no LDS, half the unrolled pass of the 32-chunk kernel.
@@ -753,9 +759,10 @@ constexpr int RES_PCS_RW = 16, RES_PCS_RX = 16, RES_PCS_LX = 0;
 // on chip, 16 per double2 of w alone, 32 per streamed double2) under the
 // column-cache variant: the cached pairs, the rest of the register-held w, the
 // streamed rest.
-i64 pc_bytes(i64 n2, int G) {
+i64 pc_bytes(i64 n2, int G, bool hh) {
     if (RES_PCS && n2 <= (i64)G * RES_PCS_RW * RES_PC_NT) return 8 * n2;  // the 16-chunk kernel: all cached
-    const i64 cap = (i64)G * RES_PC_RW * RES_PC_NT, cached = (i64)G * (RES_PC_RX + RES_PC_LX) * RES_PC_NT;
+    const int rx = hh ? RES_PC_RX : RES_PC_RX_MGS;
+    const i64 cap = (i64)G * RES_PC_RW * RES_PC_NT, cached = (i64)G * (rx + RES_PC_LX) * RES_PC_NT;
     const i64 r = std::min(n2, cap), c = std::min(r, cached);
     return 8 * c + 16 * (r - c) + 32 * (n2 - r);
 }
@@ -817,8 +824,8 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
     // slower on it: 11.3-11.5 vs 9.6 us, ab_wpc_touch_r04e).
     const bool pc_fits = n2 <= (i64)gmax * RES_PC_RW * RES_PC_NT;
     const i64 other_bytes = std::min(pairs_bytes(n2, gmax), wonly_bytes(n2, gmax));
-    const bool pc_pays = pc_fits && (RES_PC_NT == 512 ? pc_bytes(n2, gmax) < other_bytes
-                                                      : 3 * pc_bytes(n2, gmax) <= 2 * other_bytes);
+    const bool pc_pays = pc_fits && (RES_PC_NT == 512 ? pc_bytes(n2, gmax, hh) < other_bytes
+                                                      : 3 * pc_bytes(n2, gmax, hh) <= 2 * other_bytes);
     if (p.r2 >= need || cap < RES_R2_BIG) {
         p.G = gcw;
         p.pf = p.cw = true;
@@ -830,7 +837,7 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         p.wt = RES_PC_NT;
         spread(RES_PC_NT, RES_PC_RW, 0);
         p.pcs = RES_PCS && p.r2e <= RES_PCS_RW;
-        p.r2 = p.pcs ? RES_PCS_RX : RES_PC_RX;
+        p.r2 = p.pcs ? RES_PCS_RX : (hh ? RES_PC_RX : RES_PC_RX_MGS);
         p.l2 = p.pcs ? RES_PCS_LX : RES_PC_LX;
         p.lds = p.l2 * RES_PC_NT * (int)sizeof(double2);
         p.nt = true;
@@ -977,7 +984,7 @@ int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     if constexpr (RES_PCS) {
         if (p.pcs) return launch_wpc_k<RES_PCS_RW, RES_PCS_RX, RES_PCS_LX, MODE>(c, p, a);
     }
-    return launch_wpc_k<RES_PC_RW, RES_PC_RX, RES_PC_LX, MODE>(c, p, a);
+    return launch_wpc_k<RES_PC_RW, MODE == gk::RES_MGS ? RES_PC_RX_MGS : RES_PC_RX, RES_PC_LX, MODE>(c, p, a);
 }
 
 int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {

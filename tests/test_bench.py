@@ -88,14 +88,14 @@ def test_resident_byte_model_follows_the_variant():
     assert sum(r.values()) == n and r["pairs"] == 0 and r["streamed"] / n < 0.02
     per_pass = (bench.res_launch_bytes(p, n, 97) - bench.res_launch_bytes(p, n, 96)) / n
     assert 16.0 < per_pass < 16.4
-    # 4096^2 / 2 and 8192^2 / 8 (k_mgs_wpc, 512 threads): w in registers, 23 of its 32
-    # chunks' column cached (8 B per unknown), the other 9 read V_i too (16 B) -> 10.25 B
+    # 4096^2 / 2 and 8192^2 / 8 (k_mgs_wpc, 512 threads, the MGS step): w in registers, 25 of
+    # its 32 chunks' column cached (8 B per unknown), the other 7 read V_i too (16 B) -> 9.75 B
     n, p = _plan(4096, 2)
     assert p["variant"] == "w+column" and p["wt"] == 512
     r = bench.res_regions(p, n)
-    assert r == {"pairs": 2 * 256 * 23 * 512, "w_on_chip": 2 * 256 * 9 * 512, "streamed": 0}
+    assert r == {"pairs": 2 * 256 * 25 * 512, "w_on_chip": 2 * 256 * 7 * 512, "streamed": 0}
     per_pass = (bench.res_launch_bytes(p, n, 97) - bench.res_launch_bytes(p, n, 96)) / n
-    assert per_pass == pytest.approx(10.25)
+    assert per_pass == pytest.approx(9.75)
     # 4096^2 / 4: 16 chunks per workgroup, all cached -> 8 B per unknown
     n4, p4 = _plan(4096, 4)
     assert p4["variant"] == "w+column" and bench.res_regions(p4, n4) == {"pairs": n4, "w_on_chip": 0, "streamed": 0}

@@ -35,7 +35,8 @@ def test_production_splits(N, R, variant, r2e, l2e, nt, hh):
     assert p["l2e"] == l2e and p["nt"] == nt
     if variant == "w+column":  # 512 threads: 4 register + 19 LDS chunks of the column cached;
         # slabs of <= 16 chunks per thread: the 16-chunk kernel, the whole column in registers
-        want = (16, 0, 0) if r2e <= 16 else (4, 19, 19 * 512 * 16)
+        # (the MGS step caches 6 register chunks, the reflection chains 4)
+        want = (16, 0, 0) if r2e <= 16 else ((4 if hh else 6), 19, 19 * 512 * 16)
         assert (p["r2"], p["l2"], p["lds"], p["wt"]) == want + (512,)
     if r2e is not None:
         assert p["r2e"] == r2e

@@ -44,10 +44,10 @@ M = 95
 POINTS = [
     # (label, world, global grid, equal-load single-GPU grid, bench JSON under profiles/)
     ("4096^2 on 1 GPU", 1, 4096, 4096, "r04/bench_default_r04g.json"),
-    ("4096^2 on 2 GPUs", 2, 4096, 2896, "r04/bench_point_2896_r04k.json"),
+    ("4096^2 on 2 GPUs", 2, 4096, 2896, "r04/bench_point_2896_r04y.json"),
     ("4096^2 on 4 GPUs", 4, 4096, 2048, "r04/bench_point_2048_r04q.json"),
     ("4096^2 on 8 GPUs", 8, 4096, 1448, "r04/bench_point_1448_r04k.json"),
-    ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r04/bench_point_2896_r04k.json"),
+    ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r04/bench_point_2896_r04y.json"),
 ]
 # {"2": {"allreduce": us, "halo": us}, "4": {...}}: gk_comm_latency of same-device rehearsals
 COMM = "r04/rehearsal_comm_latency_r04d.json"
