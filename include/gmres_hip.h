@@ -371,9 +371,9 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          resident launch (its rank-total hop) instead of by a k_xchg launch
  *                          before it; 0: the launch
  *   GK_TUNE_RES_PC         column-cache variant (GK_RES_WCOL): -1 (default) where its modelled
- *                          bytes per projection are at most 2/3 of the pairs and w-only
- *                          variants' (its one-wave pass streams slower); 0 never; 1 wherever
- *                          the slab fits its registers
+ *                          bytes per projection are fewer than both the pairs and the w-only
+ *                          variants' (two-wave build; a one-wave build, GK_RES_PC_NT=256,
+ *                          needs at most 2/3 of them); 0 never; 1 wherever the slab fits
  *   GK_TUNE_SPIN_WAIT      1 (default): gk_mgs_step_wait / gk_hh_step_wait spin on the step's
  *                          event; 0: hipEventSynchronize (may sleep in the driver per step) */
 #define GK_TUNE_PROJ_NT 0
