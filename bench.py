@@ -74,14 +74,17 @@ def res_regions(plan: dict, nloc: int) -> dict:
     DT double2: 256 (w-only, w+column), 448 (prefetch, one control wave), 512
     (pairs); w+column: the plan's "wt" (512 since round 4's two-wave build)."""
     n2 = nloc // 2
-    dt = 256 if plan["variant"] in ("w-only", "w+column") else (448 if plan.get("cw") else 512)
-    if plan["variant"] in ("w-only", "w+column") and plan.get("wt"):
+    var = plan["variant"]
+    if var == "blocked":  # k_mgs_blk: the w-only build (256 threads) or a block-cache build
+        var = "w-only" if int(plan["wt"]) == 256 else "w+column"
+    dt = 256 if var in ("w-only", "w+column") else (448 if plan.get("cw") else 512)
+    if var in ("w-only", "w+column") and plan.get("wt"):
         dt = int(plan["wt"])  # threads per workgroup = double2 per chunk
     nres2 = min(int(plan["nres2"]), n2)
     nreg2 = min(nres2, int(plan["G"]) * int(plan["r2e"]) * dt)
-    if plan["variant"] == "w-only":
+    if var == "w-only":
         return {"pairs": 0, "w_on_chip": 2 * nres2, "streamed": 2 * (n2 - nres2) + (nloc & 1)}
-    if plan["variant"] == "w+column":  # w in registers; the column of r2 + l2 chunks per thread cached
+    if var == "w+column":  # w in registers; the column (blocked: each block slot) of r2 + l2 chunks cached
         cached = min(nres2, int(plan["G"]) * min(int(plan["r2e"]), int(plan["r2"]) + int(plan["l2"])) * dt)
         return {"pairs": 2 * cached, "w_on_chip": 2 * (nres2 - cached), "streamed": 2 * (n2 - nres2) + (nloc & 1)}
     return {"pairs": 2 * nreg2, "w_on_chip": 2 * (nres2 - nreg2), "streamed": 2 * (n2 - nres2) + (nloc & 1)}

@@ -35,14 +35,16 @@ GK_TUNE_GRAPH = 19
 GK_TUNE_RES_QDEF = 20
 GK_TUNE_RES_PC = 21
 GK_TUNE_RES_FOLD = 22
+GK_TUNE_RES_BLOCK = 23
+GK_TUNE_WATCHDOG_MS = 24
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 (GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES, GK_KID_PREC,
  GK_KID_HALO, GK_KID_GRAPH) = range(10)
 KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res", "prec", "halo", "graph"]
 COMM_KINDS = {0: None, 1: "rccl", 2: "local-group", 3: "xgmi-device-exchange"}
 # resident-step variants (gk_res_info / gk_res_plan_query)
-RES_VARIANTS = {0: None, 1: "prefetch", 2: "pairs", 3: "pairs+lds", 4: "w-only", 5: "w+column"}
-RES_INFO_KEYS = ["variant", "G", "r2", "l2", "pf", "cw", "wo", "nt", "r2e", "l2e", "lds", "nres2", "sten", "cheb_sten", "wt"]
+RES_VARIANTS = {0: None, 1: "prefetch", 2: "pairs", 3: "pairs+lds", 4: "w-only", 5: "w+column", 6: "blocked"}
+RES_INFO_KEYS = ["variant", "G", "r2", "l2", "pf", "cw", "wo", "nt", "r2e", "l2e", "lds", "nres2", "sten", "cheb_sten", "wt", "blk"]
 
 c_int, c_double, c_ll, c_vp = ctypes.c_int, ctypes.c_double, ctypes.c_longlong, ctypes.c_void_p
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -108,11 +110,12 @@ _SIGS = {
     "gk_profile_reset": (c_int, [c_vp]),
     "gk_profile_read": (c_int, [c_vp, c_int, _dp, ctypes.POINTER(c_ll)]),
     "gk_sync": (c_int, [c_vp]),
+    "gk_debug_hold_stream": (c_int, [c_vp, c_int]),
     "gk_profile_res_wg": (c_int, [c_vp, c_int, _dp, _dp, c_int, _ip]),
     "gk_profile_res_trace": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, _ip, _ip, _dp]),
     "gk_profile_res_split": (c_int, [c_vp, c_int, c_int, _dp, _dp, _dp, ctypes.POINTER(c_ll)]),
     "gk_set_tuning": (c_int, [c_vp, c_int, c_int]),
-    "gk_res_plan_query": (c_int, [c_ll, c_int, c_int, c_int, c_int, ctypes.POINTER(c_ll)]),
+    "gk_res_plan_query": (c_int, [c_ll, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_ll)]),
     "gk_res_info": (c_int, [c_vp, c_int, ctypes.POINTER(c_ll)]),
     "gk_lanczos_bounds": (c_int, [c_vp, c_int, _dp, _dp]),
     "gk_vec_count": (c_int, [c_vp, _ip]),

@@ -29,12 +29,14 @@ DRIVER = os.path.join(LIB, "test_mfp_hip")
 # Translation units compiled in parallel: the C-ABI + every kernel but the
 # Chebyshev pass, and the Chebyshev pass split by level count (its many
 # unrolled instantiations dominate the build time).
-HIP_SOURCES = [os.path.join(CSRC, "gk_api.hip"), os.path.join(CSRC, "gk_cheb.hip")]
+HIP_SOURCES = [os.path.join(CSRC, "gk_api.hip"), os.path.join(CSRC, "gk_cheb.hip"), os.path.join(CSRC, "gk_blk.hip")]
 # (source, extra defines, object name): the Chebyshev pass in GK_CF_PARTS parts
 GK_CF_PARTS = 4
-HIP_UNITS = [(HIP_SOURCES[0], [], "gk_api.o")] + [(HIP_SOURCES[1], [f"GK_CF_PART={p}"], f"gk_cheb{p}.o")
-                                                   for p in range(GK_CF_PARTS)]
-HIP_HEADERS = [os.path.join(CSRC, h) for h in ("gk_common.hpp", "gk_kernels.hpp", "gk_cheb.hpp")]
+HIP_UNITS = ([(HIP_SOURCES[0], [], "gk_api.o")] + [(HIP_SOURCES[1], [f"GK_CF_PART={p}"], f"gk_cheb{p}.o")
+                                                    for p in range(GK_CF_PARTS)]
+             + [(HIP_SOURCES[2], [], "gk_blk.o")])
+HIP_HEADERS = [os.path.join(CSRC, h) for h in ("gk_common.hpp", "gk_kernels.hpp", "gk_cheb.hpp", "gk_res.hpp",
+                                                "gk_blk.hpp")]
 HIP_DEPS = HIP_SOURCES + HIP_HEADERS + [os.path.join(ROOT, "include", "gmres_hip.h")]
 HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
 F_SOURCES = [os.path.join(FSRC, "gmres_hip.f90")]
@@ -97,7 +99,7 @@ def _compile_link(so: str, defines: list[str]) -> None:
     for p in procs:
         err = p.communicate()[1]
         sys.stderr.write("".join(l + "\n" for l in err.splitlines() if "warning:" in l or "error" in l))
-        for name in ("k_cheb_fused", "k_mgs_wpc", "k_mgs_wres", "k_mgs_res"):
+        for name in ("k_cheb_fused", "k_mgs_wpc", "k_mgs_wres", "k_mgs_res", "k_mgs_blk"):
             bad += _scratch_kernels(err, name)
     if any(p.returncode for p in procs):
         raise subprocess.CalledProcessError(max(p.returncode for p in procs), "hipcc")

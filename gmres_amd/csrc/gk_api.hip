@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/gmres_hip.h"
+#include "gk_blk.hpp"
 #include "gk_kernels.hpp"
 
 using gk::i64;
@@ -130,7 +131,12 @@ struct gk_ctx {
     int xs_timeout_ms = 20000;
     gk::u64 xs_timeout = 0;
     // resident MGS-R step (gk::k_mgs_res): one persistent launch per Arnoldi step
-    gk::u64 *res_gath = nullptr;                    // [2][RGMAX][2] all-gather granules
+    gk::u64 *res_gath = nullptr;                    // [RES_KMAX values][2][RGMAX][2] all-gather granules
+    double *res_gm = nullptr;                       // blocked step: the cycle's Gram table [m+1][RES_SMAX]
+    int tune_res_blk = 1;                           // blocked-projection MGS step: S (1 = strict MGS-R)
+    int watchdog_ms = 0;                            // host watchdog of stream waits (0: from the device deadlines)
+    bool broken = false;                            // the watchdog fired: a kernel of this context never completed
+    unsigned *hold_word = nullptr, *hold_word_dev = nullptr;  // gk_debug_hold_stream's mapped word
     int *res_err = nullptr, *res_err_dev = nullptr;  // mapped deadline flag
     unsigned res_tag = 1;                           // next granule tag (never 0)
     int res_cus = 0;                                // compute units of the device
@@ -333,7 +339,10 @@ int res_check(gk_ctx *c) {
 // more processes / streams on a device than its hardware queues) would keep the
 // host waiting forever.  Past twice the longest device deadline plus a minute,
 // the wait fails with GK_ERR_COMM instead.
-long long watchdog_ms(const gk_ctx *c) { return 2LL * std::max(c->res_timeout_ms, c->xs_timeout_ms) + 60000; }
+// GK_TUNE_WATCHDOG_MS overrides the limit (tests; a deployment that knows its queue drains).
+long long watchdog_ms(const gk_ctx *c) {
+    return c->watchdog_ms > 0 ? (long long)c->watchdog_ms : 2LL * std::max(c->res_timeout_ms, c->xs_timeout_ms) + 60000;
+}
 
 int spin_until(gk_ctx *c, hipError_t (*query)(void *), void *obj, const char *what) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -344,11 +353,16 @@ int spin_until(gk_ctx *c, hipError_t (*query)(void *), void *obj, const char *wh
         if ((it & 1023u) == 0) {
             const long long ms = std::chrono::duration_cast<std::chrono::milliseconds>(
                                      std::chrono::steady_clock::now() - t0).count();
-            if (ms > watchdog_ms(c))
+            if (ms > watchdog_ms(c)) {
+                // work is still queued on the stream: the context cannot be used (or its
+                // buffers freed) safely any more -- every later call fails, gk_destroy
+                // frees only once the stream has drained
+                c->broken = true;
                 return set_err(GK_ERR_COMM,
                                "%s: not complete after %lld ms (rank %d of %d): a kernel of this context was never "
-                               "scheduled -- more streams on the device than hardware queues?",
+                               "scheduled -- more streams on the device than hardware queues?  The context is broken.",
                                what, ms, c->rank, c->nranks);
+            }
         }
     }
 }
@@ -701,6 +715,8 @@ struct ResPlan {
     bool pf = false, nt = false, cw = false, wo = false;
     bool pc = false;       // column-cache variant (k_mgs_wpc): w in registers, running column cached
     bool pcs = false;      // ... its 16-chunk instantiation (whole column in registers)
+    int blk = 0;           // > 1: the blocked-projection MGS step k_mgs_blk with blocks of `blk` (gk_blk.hpp)
+    int bvar = -1;         // ... its instantiation (gk::BLK_*)
     int wt = 0;            // threads per workgroup = double2 per chunk (set by plan_resident)
     i64 nres2 = 0;
     int lds = 0;
@@ -794,7 +810,7 @@ bool wonly_pays(i64 n2, int G) { return wonly_bytes(n2, G) < pairs_bytes(n2, G);
 //   else w and the running column in 2 x 12 registers, plus (GK_TUNE_RES_LDS)
 //   w of 18 more chunks per workgroup in LDS, the rest streamed.
 void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bool hh, bool nt, ResPlan &p,
-                   int tune_pc = -1) {
+                   int tune_pc = -1, int tune_blk = 1) {
     const i64 n2 = nloc / 2;
     const i64 dcw = gk::RT - 64;
     // small vectors: no more workgroups than two chunks each (a cheaper all-gather)
@@ -822,6 +838,23 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
     // profiles/r04/ab_pc512_r04j.jsonl).  The one-wave build streamed at ~4.7 TB/s
     // to k_mgs_res's ~6.8, so there it had to save a third of the bytes (2048^2 was
     // slower on it: 11.3-11.5 vs 9.6 us, ab_wpc_touch_r04e).
+    if (!hh && tune_blk > 1) {
+        // the blocked-projection MGS step (opt-in): the instantiation by the chunks of
+        // 512 double2 a workgroup holds -- w in registers (+ LDS for the w-only build)
+        // and blocks of S columns cached where they fit (gk_blk.hpp)
+        p.G = gmax;
+        const int var = gk::blk_variant((n2 + (i64)gmax * 512 - 1) / ((i64)gmax * 512));
+        const gk::BlkGeom g = gk::blk_geom(var, tune_blk);
+        p.blk = tune_blk;
+        p.bvar = var;
+        p.wt = g.nt;
+        spread(g.nt, g.rw, g.lw);
+        p.r2 = g.rx;
+        p.l2 = g.lx;
+        p.lds = (g.lw + tune_blk * g.lx) * g.nt * (int)sizeof(double2);
+        p.nt = true;
+        return;
+    }
     const bool pc_fits = n2 <= (i64)gmax * RES_PC_RW * RES_PC_NT;
     const i64 other_bytes = std::min(pairs_bytes(n2, gmax), wonly_bytes(n2, gmax));
     const bool pc_pays = pc_fits && (RES_PC_NT == 512 ? pc_bytes(n2, gmax, hh) < other_bytes
@@ -882,18 +915,21 @@ bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
     const int gmax = std::max(1, std::min(gk::RGMAX, c->res_cus / std::max(1, c->res_share)));
     const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : RES_R2_BIG;
     plan_resident(c->nloc, gmax, cap, c->tune_res_lds, c->tune_res_wonly, hh,
-                  c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p, c->tune_res_pc);
+                  c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p, c->tune_res_pc, c->tune_res_blk);
     return true;
 }
 
 // gk_res_plan_query / gk_res_info layout
 enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, RPI_R2E, RPI_L2E, RPI_LDS, RPI_NRES2, RPI_STEN,
-       RPI_CHEB_STEN, RPI_WT };
+       RPI_CHEB_STEN, RPI_WT, RPI_BLK };
 void plan_info(const ResPlan &p, bool on, long long *info) {
     for (int k = 0; k < GK_RES_INFO_LEN; ++k) info[k] = 0;
     if (!on) return;
-    info[RPI_VARIANT] = p.pc ? GK_RES_WCOL
-                             : (p.wo ? GK_RES_WONLY : (p.pf ? GK_RES_PREFETCH : (p.l2 > 0 ? GK_RES_PAIRS_LDS : GK_RES_PAIRS)));
+    info[RPI_VARIANT] = p.blk > 1 ? GK_RES_BLOCKED
+                        : p.pc    ? GK_RES_WCOL
+                                  : (p.wo ? GK_RES_WONLY
+                                          : (p.pf ? GK_RES_PREFETCH : (p.l2 > 0 ? GK_RES_PAIRS_LDS : GK_RES_PAIRS)));
+    info[RPI_BLK] = p.blk > 1 ? p.blk : 1;
     info[RPI_G] = p.G;
     info[RPI_R2] = p.r2;
     info[RPI_L2] = p.l2;
@@ -988,6 +1024,14 @@ int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 }
 
 int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
+    if (p.blk > 1) {
+        if (a.mode != gk::RES_MGS) return set_err(GK_ERR_STATE, "the blocked step is the MGS-R step's only");
+        const int e = gk::blk_launch(p.bvar, p.blk, a, p.G, p.lds, c->dev, c->st);
+        if (e != 0)
+            return set_err(GK_ERR_HIP, "k_mgs_blk (S=%d, variant %d): %s", p.blk, p.bvar,
+                           hipGetErrorString(static_cast<hipError_t>(e)));
+        return GK_OK;
+    }
     if (p.wo) return launch_wres(c, p, a);
     if (p.pc) {
         switch (a.mode) {
@@ -1030,9 +1074,10 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
     if (sten_v != nullptr && (!p.wo || mode != gk::RES_MGS || c->N % 2 != 0))
         return set_err(GK_ERR_STATE, "the stencil prologue needs the w-only MGS step and even N");
     // exchanges of the launch (the stencil prologue adds the first dot's)
-    const int np = (mode == gk::RES_MGS ? 2 * j : j) + (close ? 1 : 0) + (sten_v != nullptr ? 1 : 0);
+    const int np = (mode == gk::RES_MGS ? (p.blk > 1 ? gk::blk_exchanges(j, p.blk) : 2 * j) : j) + (close ? 1 : 0) +
+                   (sten_v != nullptr ? 1 : 0);
     if (c->res_tag > 0xF0000000u) {  // tags must never repeat within the granule region's lifetime
-        HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_WORDS, c->st));
+        HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_ALL, c->st));
         c->res_tag = 1;
     }
     gk::ResArgs a{};
@@ -1048,6 +1093,7 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
     a.hs = hs;
     a.hcopy = hcopy;
     a.gath = c->res_gath;
+    a.gm = c->res_gm;
     a.j = j;
     a.n = c->nloc;
     a.nres2 = p.nres2;
@@ -1381,6 +1427,9 @@ int owner_of(gk_ctx *c, i64 gidx) {
 
 int check_ctx(gk_ctx *c) {
     if (c == nullptr) return set_err(GK_ERR_ARG, "null context");
+    if (c->broken)
+        return set_err(GK_ERR_STATE, "context broken by an earlier watchdog timeout (work never completed on its "
+                                     "stream): destroy it");
     if (c->nranks > 1 && !c->comm_ok) return set_err(GK_ERR_STATE, "communicator not initialised");
     return GK_OK;
 }
@@ -1598,10 +1647,12 @@ int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out)
         hipHostMalloc(&c->hallh, sizeof(double) * (size_t)(m + 2) * (m + 1), hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void **)&c->hallh_dev, c->hallh, 0) != hipSuccess)
         return fail(set_err(GK_ERR_NOMEM, "cannot allocate the Hessenberg mirrors"));
-    if (hipMalloc(&c->res_gath, sizeof(gk::u64) * gk::RES_GATH_WORDS) != hipSuccess ||
+    if (hipMalloc(&c->res_gath, sizeof(gk::u64) * gk::RES_GATH_ALL) != hipSuccess ||
+        hipMalloc(&c->res_gm, sizeof(double) * (size_t)(m + 1) * gk::RES_SMAX) != hipSuccess ||
         hipHostMalloc((void **)&c->res_err, sizeof(int), hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void **)&c->res_err_dev, c->res_err, 0) != hipSuccess ||
-        hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_WORDS, c->st) != hipSuccess)
+        hipMemsetAsync(c->res_gm, 0, sizeof(double) * (size_t)(m + 1) * gk::RES_SMAX, c->st) != hipSuccess ||
+        hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_ALL, c->st) != hipSuccess)
         return fail(set_err(GK_ERR_NOMEM, "cannot allocate the resident-step exchange area"));
     *c->res_err = 0;
     {
@@ -1633,6 +1684,12 @@ int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out)
 int gk_destroy(gk_ctx *c) {
     if (c == nullptr) return GK_OK;
     (void)hipSetDevice(c->dev);
+    if (c->broken && c->st) {
+        // a broken context's stream may never drain: wait a bounded time, and leak the
+        // context (rather than free memory its kernels may still touch) if it does not
+        if (spin_until(c, query_stream, c->st, "destroy of a broken context") != GK_OK)
+            return set_err(GK_ERR_COMM, "gk_destroy: the broken context's stream did not drain; its memory is kept");
+    }
     if (c->st) (void)hipStreamSynchronize(c->st);
     graph_reset(c);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -1644,6 +1701,8 @@ int gk_destroy(gk_ctx *c) {
     if (c->xs_seqdev) (void)hipFree(c->xs_seqdev);
     if (c->xs_err) (void)hipHostFree(c->xs_err);
     if (c->res_gath) (void)hipFree(c->res_gath);
+    if (c->res_gm) (void)hipFree(c->res_gm);
+    if (c->hold_word) (void)hipHostFree(c->hold_word);
     if (c->res_stamps) (void)hipFree(c->res_stamps);
     if (c->res_trace) (void)hipFree(c->res_trace);
     if (c->res_err) (void)hipHostFree(c->res_err);
@@ -1786,6 +1845,7 @@ int gk_xchg_open(gk_ctx *c, const unsigned char *handles) {
         c->xs_mapped.push_back(p);
         c->xs_peers.p[r] = static_cast<gk::u64 *>(p);
     }
+    graph_reset(c);  // captured steps hold the collective they were captured with
     c->xs_ready = true;
     c->xs_on = true;
     c->comm_ok = true;
@@ -1824,6 +1884,7 @@ int gk_xchg_local(gk_ctx *c) {
                        "GPU_MAX_HW_QUEUES >= %d before the HIP runtime starts",
                        same_dev, c->dev, q, same_dev + 1);
     for (int r = 0; r < c->nranks; ++r) c->xs_peers.p[r] = c->lg->members[r]->xs_buf;
+    graph_reset(c);
     c->xs_ready = true;
     c->xs_on = true;
     return GK_OK;
@@ -1908,6 +1969,7 @@ int gk_xchg_selftest(gk_ctx *c, int timeout_ms) {
     HIPCHK(hipSetDevice(c->dev));
     const bool was_on = c->xs_on;
     const int t_keep = c->xs_timeout_ms;
+    if (!was_on) graph_reset(c);  // graphs captured on another collective must not replay over this one
     c->xs_on = true;
     xs_set_timeout(c, timeout_ms > 0 ? timeout_ms : t_keep);
     std::string why;
@@ -1918,6 +1980,7 @@ int gk_xchg_selftest(gk_ctx *c, int timeout_ms) {
         (void)hipStreamSynchronize(c->st);
         *c->xs_err = 0;
         c->xs_on = false;
+        graph_reset(c);  //  graphs captured over the exchange would replay its k_xchg nodes
         if (c->comm == nullptr && c->lg == nullptr) c->comm_ok = c->nranks == 1;
         return set_err(GK_ERR_COMM, "device exchange self-test failed on rank %d: %s", c->rank, why.c_str());
     }
@@ -2504,6 +2567,12 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_RES_QDEF: c->tune_res_qdef = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_RES_PC: c->tune_res_pc = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_RES_FOLD: c->tune_res_fold = value != 0; break;
+        case GK_TUNE_WATCHDOG_MS: c->watchdog_ms = std::max(0, value); break;
+        case GK_TUNE_RES_BLOCK:
+            if (value != 1 && value != 2 && value != 4)
+                return set_err(GK_ERR_ARG, "GK_TUNE_RES_BLOCK %d: blocks of 1 (strict MGS-R), 2 or 4 projections", value);
+            c->tune_res_blk = value;
+            break;
         case GK_TUNE_VERR_ORDER: c->tune_verr_order = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
@@ -2655,6 +2724,24 @@ int gk_profile_res_split(gk_ctx *c, int mode, int which, double *pass_ms, double
     return GK_OK;
 }
 
+int gk_debug_hold_stream(gk_ctx *c, int hold) {
+    if (c == nullptr) return set_err(GK_ERR_ARG, "null context");
+    HIPCHK(hipSetDevice(c->dev));
+    if (c->hold_word == nullptr) {
+        HIPCHK(hipHostMalloc((void **)&c->hold_word, sizeof(unsigned), hipHostMallocMapped));
+        HIPCHK(hipHostGetDevicePointer((void **)&c->hold_word_dev, c->hold_word, 0));
+        *c->hold_word = 0;
+    }
+    if (hold) {
+        if (c->broken) return set_err(GK_ERR_STATE, "context broken");
+        __atomic_store_n(c->hold_word, 0u, __ATOMIC_RELEASE);
+        HIPCHK(hipStreamWaitValue32(c->st, c->hold_word_dev, 1u, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    } else {
+        __atomic_store_n(c->hold_word, 1u, __ATOMIC_RELEASE);
+    }
+    return GK_OK;
+}
+
 int gk_sync(gk_ctx *c) {
     CHK(check_ctx(c));
     HIPCHK(hipSetDevice(c->dev));
@@ -2663,11 +2750,12 @@ int gk_sync(gk_ctx *c) {
     return GK_OK;
 }
 
-int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, long long *info) {
-    if (info == nullptr || nloc < 2 || cus < 1 || share < 1) return set_err(GK_ERR_ARG, "bad plan query");
+int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, int block, long long *info) {
+    if (info == nullptr || nloc < 2 || cus < 1 || share < 1 || (block != 1 && block != 2 && block != 4))
+        return set_err(GK_ERR_ARG, "bad plan query");
     const int gmax = std::max(1, std::min(gk::RGMAX, cus / share));
     ResPlan p;
-    plan_resident(nloc, gmax, RES_R2_BIG, 1, -1, hh != 0, nt < 0 ? nt_auto_for(nloc) : nt != 0, p);
+    plan_resident(nloc, gmax, RES_R2_BIG, 1, -1, hh != 0, nt < 0 ? nt_auto_for(nloc) : nt != 0, p, -1, block);
     plan_info(p, true, info);
     return GK_OK;
 }

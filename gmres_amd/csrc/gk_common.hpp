@@ -39,6 +39,20 @@ __device__ __forceinline__ double reduce_slab(const double *__restrict__ p, int 
     return block_sum(s, sm);
 }
 
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+// Load policy for the Krylov-basis columns: plain, or non-temporal (`nt`) so
+// the once-per-launch V stream does not displace w from the Infinity Cache.
+template <bool NT>
+__device__ __forceinline__ double2 ldv(const double2 *p) {
+    if constexpr (NT) {
+        const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
+        return double2{t.x, t.y};
+    } else {
+        return *p;
+    }
+}
+
 // Fused reductions of a pass: none, <y, vdot>, or <y, y>.
 enum { ACC_NONE = 0, ACC_DOT = 1, ACC_NORM = 2 };
 

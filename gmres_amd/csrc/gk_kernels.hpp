@@ -19,6 +19,7 @@
 #pragma once
 #include "gk_common.hpp"
 #include "gk_cheb.hpp"
+#include "gk_res.hpp"
 
 namespace gk {
 
@@ -36,19 +37,6 @@ namespace gk {
 // --------------------------------------------------------------------------
 enum { PJ_DOT = 0, PJ_AXPY = 1, PJ_AXPY_DOT = 2, PJ_AXPY_NORM = 3 };
 
-typedef double d2v __attribute__((ext_vector_type(2)));
-
-// Load policy for the Krylov-basis columns: plain, or non-temporal (`nt`) so
-// the once-per-launch V stream does not displace w from the Infinity Cache.
-template <bool NT>
-__device__ __forceinline__ double2 ldv(const double2 *p) {
-    if constexpr (NT) {
-        const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
-        return double2{t.x, t.y};
-    } else {
-        return *p;
-    }
-}
 
 template <int MODE, bool NT = false, int U = UNR>
 __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const double *__restrict__ va,
@@ -644,72 +632,6 @@ __global__ __launch_bounds__(TPB) void k_hh_rebuild_upd(double *__restrict__ Vb,
 
 namespace gk {
 
-// --------------------------------------------------------------------------
-// Device-initiated exchange between ranks (the "xgmi" collective back-end).
-//
-// Every rank owns one receive region in uncached HBM that is mapped into every
-// peer (IPC handles across processes, plain pointers inside one process).  A
-// value travels as granules: one 8-byte word {32 data bits | 32-bit tag}
-// written by ONE system-scope 8-byte store, so a receiver that reads the tag of
-// the current exchange also reads its data -- no separate flag, no fence.
-// Slots are double-buffered by the parity of the exchange sequence number.
-// Every exchange is a rendezvous (each rank waits for the granules of every
-// rank it receives from), so no rank gets two exchanges ahead of a partner and
-// a slot is never overwritten before it has been read.  Every wait is bounded
-// by a wall-clock deadline: a missing peer sets the context's error flag
-// instead of hanging the GPU, and every later exchange returns NaN at once.
-//
-// Region layout (8-byte words):
-//   reductions  [parity 2][source rank XS_MAXR][value XS_MAXV][half 2]
-//   halo lines  [parity 2][side 2][N][half 2]   side 0: from rank-1, 1: from rank+1
-// --------------------------------------------------------------------------
-constexpr int XS_MAXR = 16;
-constexpr int XS_MAXV = 128;
-constexpr i64 XS_RED_WORDS = 2LL * XS_MAXR * XS_MAXV * 2;
-typedef unsigned long long u64;
-struct XsPeers {
-    u64 *p[XS_MAXR];
-};
-enum { XS_SLAB = 0, XS_VEC = 1, XS_BCAST = 2 };
-
-__device__ __forceinline__ void xs_put(u64 *q, unsigned seq, unsigned data) {
-    __hip_atomic_store(q, ((u64)seq << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ int xs_flag(const int *err) {
-    return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Spin until the granule at q carries `seq`: XG_OK; XG_LATE once the deadline
-// passed (the caller names the straggler); XG_ABORT when another wait of this
-// rank already failed (the sticky flag *err is set, checked every 32 unanswered
-// polls): the exchange is dead, so a doomed launch ends within microseconds
-// instead of waiting out its own deadline, and the first failure stays the one
-// reported.
-enum { XG_ABORT = -1, XG_LATE = 0, XG_OK = 1 };
-__device__ __forceinline__ int xs_get(const u64 *q, unsigned seq, u64 deadline, unsigned *data, const int *err) {
-    for (unsigned it = 1;; ++it) {
-        const u64 g = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if ((unsigned)(g >> 32) == seq) {
-            *data = (unsigned)g;
-            return XG_OK;
-        }
-        if (wall_clock64() > deadline) return XG_LATE;
-        if ((it & 31u) == 0 && xs_flag(err) != 0) return XG_ABORT;
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-
-// Which wait missed its deadline (straggler diagnostic, decoded by the host
-// into gk_last_error): code = op << 16 | (source + 1); source = the rank (or,
-// for XSE_RES_WG, the workgroup of this rank) whose granule never came.  A
-// plain store into mapped host memory (no read-modify-write over PCIe): with
-// several failing waits the last one is reported.
-enum { XSE_XCHG = 1, XSE_BCAST = 2, XSE_HALO = 3, XSE_RES_WG = 4, XSE_RES_RANK = 5 };
-__device__ __forceinline__ void xs_fail(int *err, int op, int src) {
-    __hip_atomic_store(err, (op << 16) | ((src + 1) & 0xFFFF), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // All-reduce / broadcast of a short vector, one workgroup per rank.
 //   XS_SLAB : buf[0..count) is a partial slab; each rank reduces its own slab in a
 //             fixed order, the ranks' totals are summed in rank order, and the
@@ -834,461 +756,6 @@ __global__ __launch_bounds__(TPB) void k_xhalo(const double *__restrict__ vec, i
         else if (g == XG_LATE)
             xs_fail(err, XSE_HALO, side == 0 ? rank - 1 : rank + 1);
         (side == 0 ? hlo : hhi)[e] = v;
-    }
-}
-
-// --------------------------------------------------------------------------
-// Resident MGS-R step (gmres_mgsr.f90:341-363, :384): ONE persistent launch
-// runs the whole cascade of Arnoldi step j -- 2j projections, the norm and
-// V(:,j+1) = w/h -- instead of 2j+1 launches.  The first `nres2` double2 of w,
-// and of the Krylov column the running projection needs, stay in registers
-// for the whole step, so that part of the vector moves 8 B/unknown per
-// projection (the next column) instead of k_proj's 32; the rest of the vector
-// streams exactly as in k_proj.  With PF the next column is loaded before the
-// wait for the current dot (its loads overlap the all-gather).
-//
-// The dot of each projection is all-gathered inside the launch: every
-// workgroup publishes its partial as two tagged 8-byte granules (the data is
-// the flag: cdna_hip_programming.md Guideline 16 R2 -- no fence, no counter),
-// one wave of every workgroup sweeps all G partials (8 granules in flight per
-// lane) and sums them in a fixed order, so every workgroup computes the
-// bit-identical h and the launch is deterministic.  On N ranks the rank
-// totals then travel through the device exchange regions (k_xchg's slots and
-// sequence numbers) and are summed in rank order.  Every wait is bounded by a
-// wall-clock deadline; a miss sets *err and ends the launch (results
-// poisoned, the host reports the error).  The grid must be co-resident: one
-// workgroup per CU, pinned there by its dynamic LDS.
-// Element-wise arithmetic is k_proj's / k_scale's (bit-identical); only the
-// dot summation order differs.
-// --------------------------------------------------------------------------
-constexpr int RT = 512;       // threads per resident workgroup (8 waves, 2 per SIMD)
-constexpr int RWAVES = RT / 64;
-constexpr int RGMAX = 1024;   // max workgroups of a resident launch
-constexpr int RHMAX = 512;    // max m on the resident path (H column in LDS)
-
-struct ResArgs {
-    double *w;            // w = M^-1 A V(:,j) from the operator launch; streamed part in/out
-    const double *V;      // Krylov basis, column stride ld (doubles, even)
-    double *vout;         // V(:,j+1)
-    i64 ld;
-    const double *pin;    // partial slab of <w, V(:,1)> (operator launch; all-reduced on N ranks)
-    int npin;
-    double *hs;           // H(1:j+1, j) on device
-    double *hcopy;        // mapped host mirror of H(1:j+1, j)
-    u64 *gath;            // [2][gridDim.x][2] granules
-    int *err;             // mapped error flag
-    u64 timeout;          // wall-clock ticks per wait
-    unsigned tag0;        // granule tag of exchange p = tag0 + p (never 0)
-    int j;
-    i64 n, nres2;         // local length; resident double2 prefix
-    i64 unit_e;           // RES_HH_DOWN with unit_known: local index of the input's 1.0 (-1: other rank)
-    int unit_known;       // the input vector is a unit vector: leading dot = one element, no pass
-    int r2e, l2e;         // chunks per workgroup actually resident in registers / LDS (<= the
-                          // template's R2 / L2): the resident prefix is spread evenly
-    XsPeers peers;        // nranks > 1: device exchange regions
-    int nranks, rank;
-    unsigned xseq0;       // exchange p uses sequence number xseq0 + 1 + p
-    int mode;             // RES_MGS / RES_HH_UP / RES_HH_DOWN (res_col)
-    double coef;          // AXPY coefficient: w -= (coef*h) V_i (1 for MGS, 2 for reflections)
-    i64 tail0;            // RES_HH_UP: the closing norm counts local indices >= tail0
-    u64 *stamps;          // profiling (nullptr = off): [mode][workgroup][pass, wait, total, launches] ticks
-    // w-only kernel (k_mgs_wres) only:
-    int close_hh;         // RES_HH_UP: the launch also makes the next reflector (gmres_hh.f90:306-318):
-                          // w(1:j) = 0, w(j+1) += sign, P(:,j+1) = w / ||w|| to vout (w not written back)
-    double *hb;           // close_hh: w(1:j+1) before the fix-up, written by the owner rank (pivot input)
-    int unit_init;        // RES_HH_DOWN with unit_known: the launch builds e_u itself (w not read)
-    u64 *trace;           // gk_profile_res_trace (nullptr = off): [workgroup][RES_TRACE_X][publish, seen] ticks
-    // w-only kernel, RES_MGS with STEN: the launch forms w = A V(:,j) itself
-    const double *sten_v;         // V(:,j)
-    const double *slo, *shi;      // its halo lines -1 / nlines (nullptr: the physical boundary)
-    int N, nlines;                // grid side, slab lines
-    // k_mgs_res with NT: the LDS-held and streamed parts load their dot column V_q
-    // with the default policy (it is the next pass's AXPY column V_i: then an
-    // Infinity-Cache hit), V_i non-temporal -- the w-only kernel's policy
-    int qdef;
-    int pin_local;        // N ranks, MGS: pin is this rank's partial slab only (res_pin_fold)
-};
-constexpr int RES_TRACE_X = 2 * RHMAX + 2;  // exchanges recorded per workgroup (all of one launch)
-
-// Time split of a resident launch (gk_profile_res_split): thread 0 of each
-// workgroup accumulates wall-clock ticks spent streaming its passes and waiting
-// in the all-gathers into its own slot (no contention, plain adds).
-struct ResClock {
-    u64 t0 = 0, tp = 0, pass = 0, wait = 0;
-    __device__ __forceinline__ void start(const u64 *st) {
-        if (st != nullptr) t0 = tp = wall_clock64();
-    }
-    __device__ __forceinline__ void passed(const u64 *st) {  // a pass ended, its exchange starts
-        if (st != nullptr) {
-            const u64 n = wall_clock64();
-            pass += n - tp;
-            tp = n;
-        }
-    }
-    __device__ __forceinline__ void waited(const u64 *st) {  // the exchange returned
-        if (st != nullptr) {
-            const u64 n = wall_clock64();
-            wait += n - tp;
-            tp = n;
-        }
-    }
-    __device__ __forceinline__ void finish(u64 *st, int mode) {
-        if (st != nullptr && threadIdx.x == 0) {
-            u64 *q = st + 4 * ((i64)mode * RGMAX + blockIdx.x);
-            q[0] += pass;
-            q[1] += wait;
-            q[2] += wall_clock64() - t0;
-            q[3] += 1;
-        }
-    }
-};
-
-// Projection sequences of a resident launch (all columns of V, stride ld):
-//  RES_MGS     gmres_mgsr.f90:341-363   2j projections i = p mod j, pre-dot from
-//              pin, closes with ||w||, V(:,j+1) = w/||w|| and H(1:j+1,j)
-//  RES_HH_UP   gmres_hh.f90:290-305     w = P_j..P_1 w: i = p (p < j), pre-dot
-//              from pin, closes with ||w(j+1:n)||^2 -> hs[0]; w back to HBM
-//  RES_HH_DOWN gmres_hh.f90:269-283     v = P_1..P_j v: i = j-1-p, the pre-dot
-//              is computed in the launch, no closing reduction; v back to HBM
-// A reflection is the projection with coef 2 (w -= 2<w,P_i> P_i).
-enum { RES_MGS = 0, RES_HH_UP = 1, RES_HH_DOWN = 2 };
-enum { RK_NONE = 0, RK_DOT = 1, RK_NORM = 2 };  // reduction closing a pass
-
-__device__ __forceinline__ int res_np(int mode, int j) { return mode == RES_MGS ? 2 * j : j; }
-__device__ __forceinline__ int res_col(int mode, int j, int p) {
-    const int np = res_np(mode, j);
-    p = p < np ? p : np - 1;
-    return mode == RES_MGS ? p % j : (mode == RES_HH_UP ? p : j - 1 - p);
-}
-
-// acc += v.x^2 + v.y^2 for the element pair of local double2 index e2; with chk
-// only the elements at local index >= tail0.  tail0 <= j <= RHMAX lies inside the
-// first chunk of the vector, so callers pass a uniform chk that is true for that
-// chunk only (RES_HH_UP): the per-element test stays out of every other chunk,
-// and out of the register allocation of the steady-state loop.
-__device__ __forceinline__ void sq_acc(double &acc, const double2 &v, i64 e2, i64 tail0, bool chk) {
-    if (chk) {
-        if (2 * e2 >= tail0) acc = acc + v.x * v.x;
-        if (2 * e2 + 1 >= tail0) acc = acc + v.y * v.y;
-    } else {
-        acc = acc + v.x * v.x;
-        acc = acc + v.y * v.y;
-    }
-}
-
-__device__ __forceinline__ double block_sum_rt(double v, double *sm) {
-    v = wave_sum(v);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    __syncthreads();
-    if (lane == 0) sm[wid] = v;
-    __syncthreads();
-    double r = sm[0];
-#pragma unroll
-    for (int k = 1; k < RWAVES; ++k) r += sm[k];
-    __syncthreads();  // sm is rewritten next
-    return r;
-}
-
-// Wave 0 of every workgroup: sum the workgroup's wave partials sm[0..RWAVES)
-// in order, publish that sum of exchange p as two tagged granules, sweep the
-// G partials of the grid (8 granules in flight per lane) and sum them in a
-// fixed order; on N ranks then add the rank totals in rank order.  Result in
-// bc[0]; *okf = 0 when a deadline passed (then *err is set).
-#ifndef GK_RES_XHOPS
-#define GK_RES_XHOPS 1
-#endif
-// 1: every workgroup sweeps all partials; 2: via group leaders, in the
-// small-grid kernel (k_mgs_res with a control wave) only.  A/B with one granule
-// array (profiles/r02/ab_hops_*.jsonl): two hops 4.25 vs 4.37 us per projection at
-// 1024^2 (256 readers of one array congested the flat sweep), but 10.9 vs 10.4 at
-// 2048^2 and 43.2 vs 41.6 at 4096^2.  With 8 replicas (RES_NREP) the flat sweep
-// wins at 1024^2 too: 3.85 vs 4.1 us (profiles/r02/ab_nrep_1024.jsonl).
-constexpr int RES_XHOPS = GK_RES_XHOPS;
-constexpr int RES_NG = 8;                     // groups of the two-hop all-gather (blockIdx % 8)
-constexpr int RES_MK = (2 * RGMAX / RES_NG + 63) / 64;  // granule loads per lane of a leader's sweep
-#ifndef GK_RES_NREP
-#define GK_RES_NREP 8
-#endif
-// Replicas of the granule array: every workgroup publishes its partial into all
-// RES_NREP copies (one store per lane of 2 * NREP lanes) and sweeps copy
-// blockIdx % NREP -- under round-robin dispatch the copy of its own XCD, never
-// assumed for correctness -- so each copy's lines are polled by 1/NREP of the
-// grid instead of all of it (MI355X_MICROARCH.md allgather: 256 -> 32 readers
-// -1.9 us on a 16 KB sweep).  Copies RES_REP_STRIDE words apart (a 256 B skew on
-// top of the array size, so they fall on different channels).  1 = one array.
-constexpr int RES_NREP = GK_RES_NREP;
-constexpr i64 RES_REP_STRIDE = 4 * (i64)RGMAX + 32;
-constexpr i64 RES_REP0 = 4 * (i64)RGMAX + 4 * RES_NG;  // first replica (RES_NREP > 1)
-// [2][RGMAX][2] partials + [2][NG][2] group sums + the replicas
-constexpr i64 RES_GATH_WORDS = RES_REP0 + (RES_NREP > 1 ? RES_NREP * RES_REP_STRIDE : 0);
-// rank totals of the resident launches: replica r in value slot XS_REP_STEP * r (128 B apart)
-constexpr int XS_REP_STEP = 8;
-static_assert(RES_NREP >= 1 && RES_NREP * XS_REP_STEP <= XS_MAXV, "replicas must fit the exchange value slots");
-
-#ifndef GK_RES_POLL_SLEEP
-#define GK_RES_POLL_SLEEP 16
-#endif
-#ifndef GK_RES_POLL_SLEEP_SMALL
-#define GK_RES_POLL_SLEEP_SMALL 4
-#endif
-// s_sleep units (64 clocks) between unanswered polls, per kernel: the w-only
-// large-slab kernel (RES_POLL_SLEEP) and k_mgs_res (RES_POLL_SLEEP_SMALL).  A/B with
-// one granule array (profiles/r02/ab_poll_*.jsonl): 1 / 4 / 16 / 48 -> 4096^2 42.1 / 42.1
-// / 41.7 / 41.6 us, 1024^2 4.42 / 4.45 / 4.40 / 4.81 us per projection: continuous polls
-// by early finishers slow the stragglers' streams.  With 8 replicas
-// (profiles/r02/ab_rep_*.jsonl) 4 instead of 16: 4096^2 41.8 vs 41.5 us, but 2048^2 9.57
-// vs 9.66 and 1024^2 4.12 vs 4.28 -- a poll is cheaper once 32 readers share a copy.
-constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
-#ifndef GK_RES_PUSHER_FAST
-#define GK_RES_PUSHER_FAST 1
-#endif
-// N ranks: workgroup 0, which pushes the rank total to the peers once its sweep
-// completes, polls its granules without the sleep (its detection delay is on
-// every rank's critical path; the other workgroups' is not).
-constexpr bool RES_PUSHER_FAST = GK_RES_PUSHER_FAST != 0;
-#ifndef GK_RES_SWEEP_ALL
-#define GK_RES_SWEEP_ALL 0
-#endif
-// N ranks: 1 = every workgroup sweeps the local granules (the earlier protocol),
-// 0 = only workgroup 0 does (A/B knob).  The totals are the same bits either way.
-constexpr bool RES_SWEEP_ALL = GK_RES_SWEEP_ALL != 0;
-constexpr int RES_POLL_SLEEP_SMALL = GK_RES_POLL_SLEEP_SMALL;
-#ifndef GK_RES_POLL_SLEEP_PC
-#define GK_RES_POLL_SLEEP_PC 16
-#endif
-// the column-cache kernel k_mgs_wpc (A/B knob)
-constexpr int RES_POLL_SLEEP_PC = GK_RES_POLL_SLEEP_PC;
-
-// Wave 0 of every workgroup, N ranks: the rank totals of exchange index p
-// (sequence number a.xseq0 + 1 + p).
-__device__ __forceinline__ double res_rank_sum(const ResArgs &a, int p, double acc, bool &all_ok) {
-    const int lane = threadIdx.x;
-    // Rank totals: workgroup 0 pushes this rank's total into every peer's region,
-    // once per replica (value slot XS_REP_STEP * r of its source row: a line of its
-    // own), and every workgroup reads replica blockIdx % NREP -- 1/NREP of the grid
-    // polls each line instead of all of it.  A slot is rewritten two exchanges later
-    // at the earliest, after every workgroup of every rank has read it (rendezvous).
-    const unsigned seq = a.xseq0 + 1u + (unsigned)p, par = seq & 1u;
-    if (blockIdx.x == 0) {
-        const u64 bits = (u64)__double_as_longlong(acc);
-        for (int k = lane; k < 2 * RES_NREP * a.nranks; k += 64) {
-            const int dst = k / (2 * RES_NREP), r = (k >> 1) % RES_NREP, half = k & 1;
-            xs_put(a.peers.p[dst] + (((i64)par * XS_MAXR + a.rank) * XS_MAXV + XS_REP_STEP * r) * 2 + half, seq,
-                   half ? (unsigned)(bits >> 32) : (unsigned)bits);
-        }
-    }
-    unsigned d = 0;
-    bool ok2 = true;
-    if (lane < 2 * a.nranks) {
-        const int src = lane >> 1, half = lane & 1, r = (int)(blockIdx.x % RES_NREP);
-        const int g = xs_get(a.peers.p[a.rank] + (((i64)par * XS_MAXR + src) * XS_MAXV + XS_REP_STEP * r) * 2 + half,
-                             seq, wall_clock64() + a.timeout, &d, a.err);
-        ok2 = g == XG_OK;
-        if (g == XG_LATE) xs_fail(a.err, XSE_RES_RANK, src);
-    }
-    all_ok = all_ok && __all(ok2);
-    double r = 0.0;
-    for (int q = 0; q < a.nranks; ++q) {  // rank order, as k_xchg<XS_SLAB>
-        const unsigned lo = __shfl(d, 2 * q, 64), hi = __shfl(d, 2 * q + 1, 64);
-        const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
-        r = (q == 0) ? v : r + v;
-    }
-    return r;
-}
-
-// pin_local (N ranks, the MGS step): the stencil's first-dot partial slab `pin`
-// is this rank's alone -- no k_xchg launch before the step -- and its total h
-// goes through the rank-total hop here (exchange index -1, the launch's first
-// sequence number), summed in rank order like every in-launch total.
-__device__ __forceinline__ bool res_pin_fold(const ResArgs &a, double &h, double *bc, int *okf) {
-    if (!a.pin_local) return true;
-    if (threadIdx.x < 64) {
-        bool ok = true;
-        const double r = res_rank_sum(a, -1, h, ok);
-        if (threadIdx.x == 0) {
-            bc[0] = r;
-            *okf = ok ? 1 : 0;
-        }
-    }
-    __syncthreads();
-    h = bc[0];
-    return *okf != 0;
-}
-
-// TR: the trace stamps (gk_profile_res_trace) are compiled into the MGS-R launches only
-// (the reflection kernels are at the edge of the register file).
-template <int NW = RWAVES, bool HOP2 = false, bool TR = false, int SLEEP = RES_POLL_SLEEP>
-__device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const double *sm, double *bc, int *okf) {
-    const int lane = threadIdx.x;
-    const int G = gridDim.x;
-    const unsigned tag = a.tag0 + (unsigned)p;
-    auto rep_slot = [&](int r) -> u64 * {  // granule array of exchange p in replica r
-        return a.gath + (RES_NREP > 1 ? RES_REP0 + r * RES_REP_STRIDE : 0) + (i64)(p & 1) * G * 2;
-    };
-    u64 *slot = rep_slot((int)(blockIdx.x % RES_NREP));  // the copy this workgroup sweeps
-    double s = sm[0];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) s += sm[w];
-    u64 t_pub = 0;
-    if (TR && a.trace != nullptr) t_pub = wall_clock64();
-    if (lane < 2 * RES_NREP) {  // lane 2r + h: half h of the partial into replica r
-        const u64 bits = (u64)__double_as_longlong(s);
-        const int half = lane & 1;
-        __hip_atomic_store(rep_slot(lane >> 1) + 2 * blockIdx.x + half,
-                           ((u64)tag << 32) | (half ? (unsigned)(bits >> 32) : (unsigned)bits), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const u64 deadline = wall_clock64() + a.timeout;
-    double acc = 0.0;
-    bool all_ok = true;
-    if (HOP2 && RES_XHOPS == 2 && G > 2 * RES_NG) {
-        // Two hops.  Hop 1: the leader of group g (workgroup g < RES_NG) sweeps
-        // the granules of its members g, g + NG, g + 2NG, ... (under round-robin
-        // dispatch one XCD's workgroups: same-XCD traffic, never assumed for
-        // correctness) and publishes their sum, in member order, as a granule
-        // pair.  Hop 2: every workgroup reads the NG group sums and adds them in
-        // group order.  256 readers of 16 granules instead of 256 readers of
-        // 2G: the sweep load that queued at the granules' memory channel.
-        u64 *gs = a.gath + 4 * (i64)RGMAX + (i64)(p & 1) * RES_NG * 2;
-        if ((int)blockIdx.x < RES_NG) {
-            const int g = blockIdx.x;
-            const int nmem = (G - 1 - g) / RES_NG + 1;  // members of group g
-            unsigned v[RES_MK];
-            for (;;) {
-                u64 x[RES_MK];
-#pragma unroll
-                for (int k = 0; k < RES_MK; ++k) {  // granule gi = lane + 64k of the group: member gi/2, half gi&1
-                    const int gi = lane + 64 * k, b = g + RES_NG * (gi >> 1);
-                    x[k] = __hip_atomic_load(slot + (gi < 2 * nmem ? 2 * b + (gi & 1) : 0), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-                }
-                bool ok = true;
-#pragma unroll
-                for (int k = 0; k < RES_MK; ++k) {
-                    const bool in = lane + 64 * k < 2 * nmem;
-                    v[k] = in ? (unsigned)x[k] : 0u;
-                    ok = ok && (!in || (unsigned)(x[k] >> 32) == tag);
-                }
-                if (__all(ok)) break;
-                if (wall_clock64() > deadline) {
-                    all_ok = false;
-                    int miss = 0x7FFF;
-#pragma unroll
-                    for (int k = 0; k < RES_MK; ++k) {
-                        const int gi = lane + 64 * k;
-                        if (gi < 2 * nmem && (unsigned)(x[k] >> 32) != tag) miss = min(miss, g + RES_NG * (gi >> 1));
-                    }
-                    for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, 64));
-                    if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(SLEEP);
-            }
-            double gsum = 0.0;
-#pragma unroll
-            for (int k = 0; k < RES_MK; ++k) {  // members in increasing order per lane pair
-                const unsigned o = __shfl_xor(v[k], 1, 64);
-                const unsigned lo = (lane & 1) ? o : v[k], hi = (lane & 1) ? v[k] : o;
-                if (!(lane & 1) && lane + 64 * k < 2 * nmem)
-                    gsum = gsum + __longlong_as_double((long long)(((u64)hi << 32) | lo));
-            }
-            gsum = wave_sum(gsum);
-            if (lane < 2 && all_ok) {
-                const u64 bits = (u64)__double_as_longlong(gsum);
-                __hip_atomic_store(gs + 2 * g + lane, ((u64)tag << 32) | (lane ? (unsigned)(bits >> 32) : (unsigned)bits),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        // hop 2: lanes 0 .. 2NG-1 hold the halves of the group sums
-        unsigned d = 0;
-        while (all_ok) {
-            const u64 x = __hip_atomic_load(gs + (lane < 2 * RES_NG ? lane : 0), __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-            const bool ok = lane >= 2 * RES_NG || (unsigned)(x >> 32) == tag;
-            d = (unsigned)x;
-            if (__all(ok)) break;
-            if (wall_clock64() > deadline) {
-                all_ok = false;
-                int miss = ok ? 0x7FFF : (lane >> 1);
-                for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, 64));
-                if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);  // the leader of the missing group
-                break;
-            }
-            __builtin_amdgcn_s_sleep(SLEEP);
-        }
-        double r = 0.0;
-#pragma unroll
-        for (int q = 0; q < RES_NG; ++q) {  // group order, the same instructions in every workgroup
-            const unsigned lo = __builtin_amdgcn_readlane(d, 2 * q), hi = __builtin_amdgcn_readlane(d, 2 * q + 1);
-            const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
-            r = (q == 0) ? v : r + v;
-        }
-        acc = all_ok ? r : 0.0;
-    } else if (RES_SWEEP_ALL || a.nranks == 1 || blockIdx.x == 0) {
-        // (N ranks: only workgroup 0, the pusher, needs this rank's total -- every
-        // workgroup then reads the R rank totals, its own rank's included, so the
-        // others skip the sweep and its polls stay off the stragglers' memory path.)
-        // Lane L holds granule L + 64k of each 512-granule sweep: the lo (even L)
-        // or hi (odd L) half of workgroup c0/2 + L/2 + 32k.
-        for (int c0 = 0; c0 < 2 * G && all_ok; c0 += 512) {
-            unsigned v[8];
-            for (;;) {
-                // All 8 loads unconditionally (out-of-range lanes re-read granule 0
-                // and ignore it): a per-load bounds branch made the compiler wait for
-                // each load before issuing the next -- 8 serial round trips to the
-                // point of coherence per poll instead of one.
-                u64 x[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int g = c0 + lane + 64 * k;
-                    x[k] = __hip_atomic_load(slot + (g < 2 * G ? g : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                bool ok = true;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const bool in = c0 + lane + 64 * k < 2 * G;
-                    v[k] = in ? (unsigned)x[k] : 0u;
-                    ok = ok && (!in || (unsigned)(x[k] >> 32) == tag);
-                }
-                if (__all(ok)) break;
-                if (wall_clock64() > deadline) {
-                    all_ok = false;
-                    int miss = 0x7FFF;  // the lowest workgroup whose granule never came
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int g = c0 + lane + 64 * k;
-                        if (g < 2 * G && (unsigned)(__hip_atomic_load(slot + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                    >> 32) != tag)
-                            miss = min(miss, g >> 1);
-                    }
-                    for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, 64));
-                    if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
-                    break;
-                }
-                if (RES_PUSHER_FAST && a.nranks > 1 && blockIdx.x == 0)
-                    __builtin_amdgcn_s_sleep(1);  // the rank-total pusher: push as soon as the sweep completes
-                else
-                    __builtin_amdgcn_s_sleep(SLEEP);
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {  // workgroups in increasing order per lane pair
-                const unsigned o = __shfl_xor(v[k], 1, 64);
-                const unsigned lo = (lane & 1) ? o : v[k], hi = (lane & 1) ? v[k] : o;
-                if (!(lane & 1) && c0 + lane + 64 * k < 2 * G)
-                    acc = acc + __longlong_as_double((long long)(((u64)hi << 32) | lo));
-            }
-        }
-        acc = wave_sum(acc);  // butterfly: the same value on every lane of every workgroup
-    }
-    if (all_ok && a.nranks > 1) acc = res_rank_sum(a, p, acc, all_ok);
-    if (lane == 0) {
-        bc[0] = acc;
-        *okf = all_ok ? 1 : 0;
-        if (TR && a.trace != nullptr && p < RES_TRACE_X) {
-            u64 *q = a.trace + ((i64)blockIdx.x * RES_TRACE_X + p) * 2;
-            q[0] = t_pub;
-            q[1] = wall_clock64();
-        }
     }
 }
 

@@ -10,20 +10,29 @@ processes of one node, so a rank process never imports torch and runs the
 library on the HIP runtime and RCCL it was built against.
 
 Rendezvous: rank 0 listens on an ephemeral 127.0.0.1 port and publishes
-(port, authkey) in a file named by the launch (MASTER_ADDR, MASTER_PORT and
+"port token pid" in a file named by the launch (MASTER_ADDR, MASTER_PORT and
 the launcher's pid, which torch.distributed.run's ranks share); the other
-ranks poll for that file and connect.  Every collective is a gather to rank 0
-followed by a broadcast of the result, in rank order, so all ranks see
-identical values.
+ranks poll for that file, skip it while the pid it names is not alive (a file
+left by a crashed launch), connect and present the token, which rank 0 checks
+before it counts the rank.  Every collective is a gather to rank 0 followed by
+a broadcast of the result, in rank order, so all ranks see identical values.
+
+Every wait is bounded (round 5): the connect,
+the hello, and every receive of a collective time out after `timeout` seconds
+(GK_CTL_TIMEOUT overrides the default) with a TimeoutError that names the rank
+that never answered, so a live-but-stuck peer cannot block the others forever.
 """
 from __future__ import annotations
 
 import os
+import pickle
 import secrets
+import socket
+import struct
 import tempfile
 import time
-from multiprocessing import AuthenticationError
-from multiprocessing.connection import Client, Listener
+
+_HDR = struct.Struct("!Q")
 
 
 def launch_key() -> str:
@@ -32,66 +41,145 @@ def launch_key() -> str:
                      os.environ.get("TORCHELASTIC_RUN_ID", ""), str(os.getppid())]).replace("/", "_")
 
 
+def default_timeout() -> float:
+    return float(os.environ.get("GK_CTL_TIMEOUT", "300"))
+
+
+def _pid_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    return True
+
+
+class _Link:
+    """One length-prefixed pickle stream over a connected socket; every receive
+    bounded by the socket timeout."""
+
+    def __init__(self, sock: socket.socket, who: str):
+        self.sock, self.who = sock, who
+
+    def send(self, obj) -> None:
+        data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        self.sock.sendall(_HDR.pack(len(data)) + data)
+
+    def _exact(self, n: int, timeout: float) -> bytes:
+        buf = bytearray()
+        self.sock.settimeout(timeout)
+        while len(buf) < n:
+            try:
+                chunk = self.sock.recv(n - len(buf))
+            except socket.timeout as e:
+                raise TimeoutError(f"control plane: no message from {self.who} within {timeout:.0f} s") from e
+            if not chunk:
+                raise ConnectionError(f"control plane: {self.who} closed the connection")
+            buf += chunk
+        return bytes(buf)
+
+    def recv(self, timeout: float):
+        (n,) = _HDR.unpack(self._exact(_HDR.size, timeout))
+        return pickle.loads(self._exact(n, timeout))
+
+    def close(self) -> None:
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+
+
 class Ctl:
     """A gather/broadcast control plane over TCP between the ranks of one node."""
 
-    def __init__(self, rank: int, world: int, key: str | None = None, timeout: float = 300.0,
+    def __init__(self, rank: int, world: int, key: str | None = None, timeout: float | None = None,
                  rdzv_dir: str | None = None):
         self.rank, self.world = rank, world
-        self.timeout = timeout
-        self._peers = []  # rank 0: connections of ranks 1..world-1, in rank order
-        self._conn = None  # ranks > 0: connection to rank 0
-        self._listener = None
+        self.timeout = default_timeout() if timeout is None else float(timeout)
+        self._peers: list[_Link] = []  # rank 0: links to ranks 1..world-1, in rank order
+        self._conn: _Link | None = None  # ranks > 0: link to rank 0
+        self._listener: socket.socket | None = None
         self._file = os.path.join(rdzv_dir or tempfile.gettempdir(), f"gk_ctl_{key or launch_key()}")
         if world == 1:
             return
+        deadline = time.monotonic() + self.timeout
         if rank == 0:
-            auth = secrets.token_bytes(16)
-            self._listener = Listener(("127.0.0.1", 0), authkey=auth)
-            port = self._listener.address[1]
-            tmp = self._file + f".{os.getpid()}.tmp"
-            with open(tmp, "w") as f:
-                f.write(f"{port} {auth.hex()}\n")
-            os.replace(tmp, self._file)  # atomic: a reader sees all of it or nothing
-            sock = getattr(getattr(self._listener, "_listener", None), "_socket", None)
-            if sock is not None:
-                sock.settimeout(timeout)  # accept() raises instead of waiting forever for a dead rank
-            got = {}
-            deadline = time.monotonic() + timeout
-            while len(got) < world - 1:
-                if time.monotonic() > deadline:
-                    raise TimeoutError(f"control plane: {world - 1 - len(got)} rank(s) never connected")
-                c = self._listener.accept()
-                r = c.recv()
-                got[int(r)] = c
-            self._peers = [got[r] for r in range(1, world)]
+            self._serve(deadline)
         else:
-            deadline = time.monotonic() + timeout
-            last = None
-            while True:
-                try:
-                    port, auth = open(self._file).read().split()
-                    self._conn = Client(("127.0.0.1", int(port)), authkey=bytes.fromhex(auth))
-                    self._conn.send(rank)
-                    break
-                except (OSError, ValueError, EOFError, AuthenticationError) as e:  # not published yet / a stale file
-                    last = e
-                    if time.monotonic() > deadline:
-                        raise TimeoutError(f"control plane: rank {rank} could not reach rank 0 ({last})") from e
-                    time.sleep(0.05)
+            self._join(deadline)
+
+    def _serve(self, deadline: float) -> None:
+        token = secrets.token_hex(16)
+        ls = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        ls.bind(("127.0.0.1", 0))
+        ls.listen(self.world)
+        self._listener = ls
+        tmp = self._file + f".{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
+            f.write(f"{ls.getsockname()[1]} {token} {os.getpid()}\n")
+        os.replace(tmp, self._file)  # atomic: a reader sees all of it or nothing
+        got: dict[int, _Link] = {}
+        while len(got) < self.world - 1:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                missing = sorted(set(range(1, self.world)) - set(got))
+                raise TimeoutError(f"control plane: rank(s) {missing} never connected")
+            ls.settimeout(left)
+            try:
+                s, _ = ls.accept()
+            except socket.timeout:
+                continue
+            link = _Link(s, "a connecting rank")
+            try:
+                hello = link.recv(min(10.0, max(left, 0.1)))
+            except (TimeoutError, ConnectionError, pickle.UnpicklingError, EOFError):
+                link.close()  # not one of ours (or too slow to say hello): drop it
+                continue
+            if not (isinstance(hello, tuple) and len(hello) == 2 and hello[0] == token
+                    and isinstance(hello[1], int) and 0 < hello[1] < self.world and hello[1] not in got):
+                link.close()
+                continue
+            link.who = f"rank {hello[1]}"
+            link.send("ok")
+            got[hello[1]] = link
+        self._peers = [got[r] for r in range(1, self.world)]
+
+    def _join(self, deadline: float) -> None:
+        last = None
+        while True:
+            try:
+                port, token, pid = open(self._file).read().split()
+                if not _pid_alive(int(pid)):
+                    raise ValueError(f"rendezvous file of a dead rank 0 (pid {pid})")
+                left = max(0.1, deadline - time.monotonic())
+                s = socket.create_connection(("127.0.0.1", int(port)), timeout=min(5.0, left))
+                link = _Link(s, "rank 0")
+                link.send((token, self.rank))
+                if link.recv(min(10.0, left)) != "ok":
+                    link.close()
+                    raise ConnectionError("rank 0 refused the hello")
+                self._conn = link
+                return
+            except (OSError, ValueError, EOFError, TimeoutError, ConnectionError, pickle.UnpicklingError) as e:
+                last = e  # not published yet / a stale file / rank 0 still binding
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"control plane: rank {self.rank} could not reach rank 0 ({last})") from e
+                time.sleep(0.05)
 
     # -------------------------------------------------------------- collectives
     def allgather(self, obj) -> list:
-        """Every rank's object, in rank order, on every rank."""
+        """Every rank's object, in rank order, on every rank.  A rank that does not
+        answer within the timeout raises TimeoutError naming it."""
         if self.world == 1:
             return [obj]
         if self.rank == 0:
-            vals = [obj] + [c.recv() for c in self._peers]
+            vals = [obj] + [c.recv(self.timeout) for c in self._peers]
             for c in self._peers:
                 c.send(vals)
             return vals
         self._conn.send(obj)
-        return self._conn.recv()
+        return self._conn.recv(self.timeout)
 
     def bcast(self, obj, root: int = 0):
         return self.allgather(obj if self.rank == root else None)[root]

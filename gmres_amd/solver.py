@@ -321,6 +321,11 @@ class Context:
     def sync(self) -> None:
         nat.check(nat.hip().gk_sync(self._h), "gk_sync")
 
+    def debug_hold_stream(self, hold: bool) -> None:
+        """Test hook (gk_debug_hold_stream): hold the context's stream behind a
+        never-written mapped word, or release it."""
+        nat.check(nat.hip().gk_debug_hold_stream(self._h, int(hold)), "gk_debug_hold_stream")
+
 
 def _res_dict(call, what: str) -> dict:
     buf = (nat.c_ll * len(nat.RES_INFO_KEYS))()
@@ -330,11 +335,14 @@ def _res_dict(call, what: str) -> dict:
     return d
 
 
-def res_plan_query(nloc: int, cus: int = 256, share: int = 1, hh: bool = False, nt: int = -1) -> dict:
+def res_plan_query(nloc: int, cus: int = 256, share: int = 1, hh: bool = False, nt: int = -1,
+                   block: int = 1) -> dict:
     """The resident-step variant a slab of nloc local unknowns selects on a
-    device of `cus` compute units shared by `share` contexts
-    (gk_res_plan_query: host-only, no GPU touched)."""
-    return _res_dict(lambda buf: nat.hip().gk_res_plan_query(int(nloc), int(cus), int(share), int(hh), int(nt), buf),
+    device of `cus` compute units shared by `share` contexts, with the MGS step's
+    projection block `block` (GK_TUNE_RES_BLOCK; gk_res_plan_query: host-only, no
+    GPU touched)."""
+    return _res_dict(lambda buf: nat.hip().gk_res_plan_query(int(nloc), int(cus), int(share), int(hh), int(nt),
+                                                             int(block), buf),
                      "gk_res_plan_query")
 
 

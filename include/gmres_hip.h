@@ -281,17 +281,23 @@ int gk_sync(gk_ctx *ctx);
  *                     up to 64 x 256 double2 per workgroup (one GPU of 4096^2 / 2 and
  *                     of 8192^2 / 8), in 512-thread workgroups (two waves per SIMD); slabs
  *                     of <= 16 chunks per thread (4096^2 / 4) keep the whole column in
- *                     registers (r2 = 16, l2 = 0).
+ *                     registers (r2 = 16, l2 = 0);
+ *   GK_RES_BLOCKED    k_mgs_blk (gmres_amd/csrc/gk_blk.hpp): the blocked-projection MGS-R
+ *                     step of GK_TUNE_RES_BLOCK > 1 -- one all-gather per block of S
+ *                     projections; r2 / l2 = cached column chunks per block slot in
+ *                     registers / LDS, blk = S.
  * info[GK_RES_INFO_LEN]: variant, workgroups G, R2, L2, prefetch, control
  * wave, w-only, non-temporal column loads, register / LDS chunks per
  * workgroup in use, dynamic LDS bytes, resident double2 of the slab, and
  * (gk_res_info only) whether the MGS step launch forms w = A V(:,j) itself,
  * and whether the Arnoldi step's Chebyshev(k) pass forms z = A v in its own
  * stage 0 (1 / 0; -1 on a multi-rank context whose smallest slab is not known
- * until its first solve), and the threads per workgroup (= double2 per chunk).
+ * until its first solve), the threads per workgroup (= double2 per chunk), and the
+ * projection block S (1: strict MGS-R).
  * gk_res_plan_query: pure host computation for a slab of nloc unknowns on a
  * device with `cus` compute units shared by `share` contexts; hh != 0 the
- * reflection chains' plan; nt: -1 auto (from nloc), 0 / 1 forced.  No device
+ * reflection chains' plan; nt: -1 auto (from nloc), 0 / 1 forced; block: the
+ * GK_TUNE_RES_BLOCK value (1, 2 or 4) of the MGS step's plan.  No device
  * is touched (the CPU tests pin every production split with it).
  * gk_res_info: the plan this context uses now (its tuning, communicator and
  * sharing applied); variant GK_RES_NONE when steps run launch by launch. */
@@ -301,8 +307,9 @@ int gk_sync(gk_ctx *ctx);
 #define GK_RES_PAIRS_LDS 3
 #define GK_RES_WONLY 4
 #define GK_RES_WCOL 5
-#define GK_RES_INFO_LEN 15
-int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, long long *info);
+#define GK_RES_BLOCKED 6
+#define GK_RES_INFO_LEN 16
+int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, int block, long long *info);
 int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 
 /* Launch-policy knobs (defaults are the tuned values; for A/B measurement).
@@ -374,6 +381,23 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          bytes per projection are fewer than both the pairs and the w-only
  *                          variants' (two-wave build; a one-wave build, GK_RES_PC_NT=256,
  *                          needs at most 2/3 of them); 0 never; 1 wherever the slab fits
+ *   GK_TUNE_RES_BLOCK      1 (default): the strict MGS-R step (gmres_mgsr.f90:341-360), one
+ *                          in-launch all-gather per projection; 2 or 4 (opt-in): the blocked
+ *                          step k_mgs_blk -- the projections of each sweep in blocks of S
+ *                          columns, ONE all-gather per block carrying its S dots and the Gram
+ *                          terms of its newest column, the h formed by MGS's exact-arithmetic
+ *                          recurrence h_k = <w,V_k> - sum_{l<k} h_l <V_l,V_k> (the two sweeps
+ *                          stay separate, so the reorthogonalisation still sees w after the
+ *                          whole first sweep): 2 (1 + ceil((j-1)/S)) all-gathers per step
+ *                          instead of 2j.  Not bit-identical to the strict step (within the
+ *                          residual-history tolerance of DESIGN.md 4.3).  MGS-R resident
+ *                          steps only; Householder and the launch path stay strict.
+ *   GK_TUNE_WATCHDOG_MS    limit of every host wait on the context's stream (gk_sync, the step
+ *                          waits, gk_update_x ...); 0 (default) = twice the longest device
+ *                          deadline plus a minute.  Past it the wait returns GK_ERR_COMM (a
+ *                          kernel of the context was never scheduled) and the context is
+ *                          BROKEN: every later call returns GK_ERR_STATE; gk_destroy frees it
+ *                          once its stream drains (bounded by the same limit; else it is kept)
  *   GK_TUNE_SPIN_WAIT      1 (default): gk_mgs_step_wait / gk_hh_step_wait spin on the step's
  *                          event; 0: hipEventSynchronize (may sleep in the driver per step) */
 #define GK_TUNE_PROJ_NT 0
@@ -399,7 +423,14 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_RES_QDEF 20
 #define GK_TUNE_RES_PC 21
 #define GK_TUNE_RES_FOLD 22
+#define GK_TUNE_RES_BLOCK 23
+#define GK_TUNE_WATCHDOG_MS 24
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
+/* Test hook: hold = 1 enqueues on the context's stream a wait for a mapped host
+ * word that only hold = 0 writes (hipStreamWaitValue32) -- every later kernel of
+ * the context then stays unscheduled until the release, as with a hardware queue
+ * that is never mapped; it exercises the host watchdog (GK_TUNE_WATCHDOG_MS). */
+int gk_debug_hold_stream(gk_ctx *ctx, int hold);
 
 /* ------------------------- stateless kernel API (caller device memory) ---- */
 /* y = A x on lines [0,nlines) of an N-wide slab; halo_lo / halo_hi are the

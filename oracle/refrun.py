@@ -121,7 +121,9 @@ def run(solver: str, N: int, m: int, prec: str = "identity", threads: int = 1, m
             elif k == "XERR":
                 r.x_err = (float(t[1]), float(t[2]))
             elif k == "KRYLOV":
-                r.krylov = (int(t[1]), float(t[2]))
+                # a truncated pbicgstab_omp run returns max_iter from an uninitialised
+                # local (src/bicgstab.f90:182): the I8 field then prints as stars
+                r.krylov = (int(t[1]) if t[1].lstrip("-").isdigit() else -1, float(t[2]))
         if want_x and not r.cut:
             r.x = np.fromfile(xf, dtype=np.float64)
     return r

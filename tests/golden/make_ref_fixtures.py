@@ -66,7 +66,51 @@ THREADED = [
     ("mgsr_omp_identity_1024_m95_12cyc_t8", "mgsr_omp", 1024, 95, "identity", 8, 12),
     ("mgsr_omp_cbpr2_1024_m95_12cyc_t8", "mgsr_omp", 1024, 95, "cbpr2", 8, 12),
     ("hh_omp_identity_1024_m95_12cyc_t8", "hh_omp", 1024, 95, "identity", 8, 12),
+    # round 5: the grids whose per-workgroup load stands for the 2 / 4 / 8-GPU splits
+    # (tests/test_gpu_splits.py), cycle 1 of the reference itself
+    ("mgsr_omp_identity_1448_m95_1cyc_t8", "mgsr_omp", 1448, 95, "identity", 8, 1),
+    ("mgsr_omp_identity_2048_m95_1cyc_t8", "mgsr_omp", 2048, 95, "identity", 8, 1),
+    ("mgsr_omp_identity_2896_m95_1cyc_t8", "mgsr_omp", 2896, 95, "identity", 8, 1),
+    ("hh_omp_identity_1448_m95_1cyc_t8", "hh_omp", 1448, 95, "identity", 8, 1),
+    ("hh_omp_identity_2048_m95_1cyc_t8", "hh_omp", 2048, 95, "identity", 8, 1),
+    ("hh_omp_identity_2896_m95_1cyc_t8", "hh_omp", 2896, 95, "identity", 8, 1),
 ]
+# round 5: pcg_omp / pbicgstab_omp residual HISTORIES (src/cg.f90:154-234,
+# src/bicgstab.f90:91-182).  The reference records no history, so it is taken
+# by truncation: the solver run from x0 = 0 with max_iter = k returns the
+# residual of iteration k (one serial process per k: pbicgstab_omp reads its
+# dot accumulators uninitialised, so no two runs share a process).
+KHIST = [
+    ("pcg_omp_identity_128_hist", "pcg_omp", 128, "identity"),
+    ("pcg_omp_cbpr2_128_hist", "pcg_omp", 128, "cbpr2"),
+    ("pbicgstab_omp_identity_128_hist", "pbicgstab_omp", 128, "identity"),
+    ("pbicgstab_omp_cbpr2_128_hist", "pbicgstab_omp", 128, "cbpr2"),
+    ("pcg_omp_identity_256_hist", "pcg_omp", 256, "identity"),
+    ("pcg_omp_cbpr2_256_hist", "pcg_omp", 256, "cbpr2"),
+    ("pbicgstab_omp_identity_256_hist", "pbicgstab_omp", 256, "identity"),
+    ("pbicgstab_omp_cbpr2_256_hist", "pbicgstab_omp", 256, "cbpr2"),
+]
+
+
+def hist_points(K: int) -> list[int]:
+    """Iterations of a truncation history: every one."""
+    return list(range(1, K + 1))
+
+
+def record_khist(key, solver, N, prec):
+    t0 = time.time()
+    full = refrun.run(solver, N, 5000, prec, threads=1)
+    K, res = full.krylov
+    pts = hist_points(K)
+    with ThreadPoolExecutor(6) as ex:
+        hist = list(ex.map(lambda k: refrun.run(solver, N, k, prec, threads=1).krylov[1], pts))
+    d = {"solver": solver, "N": N, "m": 5000, "prec": prec, "threads": 1, "cut": False, "tol": 1e-9, "iterations": K,
+         "res": res,
+         "hist_iter": pts, "hist_res": hist, "x_err": list(full.x_err),
+         "note": "hist_res[i] = the reference's residual after hist_iter[i] iterations (run truncated there)",
+         "wall_s": round(time.time() - t0, 2)}
+    print(f"{key}: {K} iterations, {len(pts)} history points, {time.time() - t0:.1f} s", flush=True)
+    return key, d
 
 
 def record(key, solver, N, m, prec, threads, max_cycles):
@@ -89,7 +133,7 @@ def main() -> None:
     only = None
     if "--only" in sys.argv:
         only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
-        unknown = only - {c[0] for c in SMALL + THREADED}
+        unknown = only - {c[0] for c in SMALL + THREADED + KHIST}
         if unknown:
             raise SystemExit(f"unknown cases {sorted(unknown)}")
     refrun.build()
@@ -107,6 +151,11 @@ def main() -> None:
         out[key] = d
         if x is not None:
             xs[key] = x
+    for c in KHIST:
+        if (quick and c[2] > 128) or (only is not None and c[0] not in only):
+            continue
+        key, d = record_khist(*c)
+        out[key] = d
     meta = {"_source": "oracle/_ref/ref_driver: the reference's own src/*.f90 (AlexanderGSC/gmres) compiled "
                        "by oracle/Makefile.ref (amdflang 22, -O3 -fopenmp -funroll-loops; interfaces.f90 "
                        "with the one-line import fix), driven through the stencil_vector/precond seam by "

@@ -4,8 +4,10 @@ and the CPU-baseline extrapolation."""
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -240,6 +242,65 @@ def test_control_plane_world_size(world, tmp_path):
         assert o["all"] == [10 * k for k in range(world)] and o["b"] == "root"
         assert o["min"] == 1 and o["max"] == world - 0.5 and o["sum"] == world * (world - 1) // 2
     assert not os.path.exists(os.path.join(str(tmp_path), "gk_ctl_t"))  # rank 0 removed the rendezvous file
+
+
+def _ctl_stuck_rank(rank, world, key, d, q):
+    """Rank 1 joins and then never takes part in a collective (a live but stuck peer)."""
+    from gmres_amd.ctl import Ctl
+
+    c = Ctl(rank, world, key=key, timeout=3, rdzv_dir=d)
+    if rank == 0:
+        t0 = time.monotonic()
+        try:
+            c.allgather(0)
+            q.put(("no error", 0.0))
+        except TimeoutError as e:
+            q.put((str(e), time.monotonic() - t0))
+    else:
+        time.sleep(8)
+    c.close()
+
+
+def test_control_plane_bounds_a_stuck_peer(tmp_path):
+    """Every control-plane receive is bounded: rank 0's
+    gather from a rank that joined but never answers fails within the timeout,
+    naming that rank, instead of blocking forever."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ctl_stuck_rank, args=(r, 2, "stuck", str(tmp_path), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    msg, dt = q.get(timeout=60)
+    for p in ps:
+        p.join(timeout=30)
+    assert "rank 1" in msg and dt < 6, (msg, dt)
+
+
+def test_control_plane_skips_a_stale_rendezvous_file(tmp_path):
+    """A rendezvous file left by a crashed launch (its rank 0 dead) is not
+    connected to: the joining rank waits for the live rank 0's file."""
+    import multiprocessing as mp
+
+    p0 = subprocess.Popen([sys.executable, "-c", "pass"])
+    p0.wait()
+    dead = p0.pid
+    with socket.socket() as s:  # a port nobody listens on after this
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    (tmp_path / "gk_ctl_stale").write_text(f"{port} {'0' * 32} {dead}\n")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    r1 = ctx.Process(target=_ctl_rank, args=(1, 2, "stale", str(tmp_path), q))
+    r1.start()
+    time.sleep(1.0)  # rank 1 polls the stale file meanwhile
+    r0 = ctx.Process(target=_ctl_rank, args=(0, 2, "stale", str(tmp_path), q))
+    r0.start()
+    got = dict(q.get(timeout=60) for _ in range(2))
+    for p in (r0, r1):
+        p.join(timeout=30)
+    assert got[0]["all"] == got[1]["all"] == [0, 10]
 
 
 def test_pmc_lookup_by_variant_and_slab():

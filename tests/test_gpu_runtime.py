@@ -97,3 +97,54 @@ def test_xchg_local_refuses_ranks_beyond_the_hardware_queues():
     # with enough queues the same group is accepted
     p = _child(REFUSE, env={"GPU_MAX_HW_QUEUES": "8"})
     assert p.returncode == 0 and p.stdout.strip().splitlines()[-1] == "ACCEPTED", (p.stdout, p.stderr[-2000:])
+
+
+def test_watchdog_bounds_a_stream_that_never_drains():
+    """The host watchdog of every stream wait: a context
+    whose stream is held behind a never-written mapped word (gk_debug_hold_stream,
+    as when its hardware queue is never mapped) fails gk_sync with GK_ERR_COMM
+    inside the GK_TUNE_WATCHDOG_MS bound, naming the cause; the context is then
+    broken (later calls refuse) and, once released, is destroyed cleanly; a solve
+    queued behind the hold fails within the bound too."""
+    import time
+
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+
+    c = ga.Context(64, 10)
+    try:
+        c.tune(nat.GK_TUNE_WATCHDOG_MS, 1500)
+        c.set_rhs_ones()
+        c.sync()
+        c.debug_hold_stream(True)
+        t0 = time.monotonic()
+        with pytest.raises(nat.GkError) as e:
+            c.sync()
+        dt = time.monotonic() - t0
+        assert "never scheduled" in str(e.value) and "status -6" in str(e.value), str(e.value)
+        assert 1.4 < dt < 10, dt
+        with pytest.raises(nat.GkError) as e2:
+            c.set_rhs_ones()
+        assert "broken" in str(e2.value)
+    finally:
+        c.debug_hold_stream(False)  # the stream drains; destroy then frees normally
+        c.close()
+    # a solve whose first kernels queue behind a hold: the Fortran host's step
+    # wait fails within the bound instead of waiting forever
+    c = ga.Context(64, 10)
+    try:
+        c.tune(nat.GK_TUNE_WATCHDOG_MS, 1500)
+        c.set_rhs_ones()
+        c.sync()
+        c.debug_hold_stream(True)
+        t0 = time.monotonic()
+        with pytest.raises(nat.GkError):
+            ga.gmres_mgsr(c, 1e-15, max_cycles=1, want_verr=False)
+        assert time.monotonic() - t0 < 15
+    finally:
+        c.debug_hold_stream(False)
+        c.close()
+    with ga.Context(64, 10) as c:  # the device is sane afterwards
+        c.set_rhs_ones()
+        r = ga.gmres_mgsr(c, 1e-15, max_cycles=2, want_verr=False)
+        assert r.n_out == 10

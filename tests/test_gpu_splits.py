@@ -19,7 +19,8 @@ R: 1448^2 ~ 4096^2 / 8, 2048^2 ~ 4096^2 / 4, 2896^2 ~ 4096^2 / 2 and
 8192^2 / 8, 4096^2 ~ the single-GPU bench.
 
 Check: one GMRES(95) cycle (MGS-R and Householder) against a single-context
-run of the same grid -- cycle-1 true residual to 1e-9, final_err(1:95) to
+run of the same grid AND against the reference's own cycle 1 at that grid
+(round 5 fixtures) -- cycle-1 true residual to 1e-9, final_err(1:95) to
 1e-6, x to 1e-9 (tolerances of tests/test_gpu_configs.py; the two runs differ
 only in the dot-product summation order) -- with the selected variant and
 workgroup count asserted, every Arnoldi step a resident launch, no
@@ -82,7 +83,18 @@ def _tune_forced(c, nt, R):
     c.tune(nat.GK_TUNE_PROJ_NT, nt)
 
 
-def _compare(ref, res, xs):
+def _ref_cycle1(N, method):
+    """The REFERENCE's own cycle-1 true residual at this grid (oracle/_ref, 8
+    threads; tests/golden/make_ref_fixtures.py, round 5 for 1448^2 / 2048^2 /
+    2896^2) -- gmres_mgsr.f90:309-413, gmres_hh.f90:211-385."""
+    import json
+    import os
+
+    runs = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_runs.json")))
+    return runs[f"{method}_omp_identity_{N}_m95_1cyc_t8"]["hist_res"][0]
+
+
+def _compare(ref, res, xs, N=None, method=None):
     assert len({(r.n_out, r.cycles_out, r.n_cycles) for r in res}) == 1
     assert all(np.array_equal(res[0].hist_res, r.hist_res) for r in res)
     assert all(np.array_equal(res[0].final_err, r.final_err) for r in res)
@@ -90,6 +102,8 @@ def _compare(ref, res, xs):
     assert res[0].hist_res[0] == pytest.approx(ref.hist_res[0], rel=1e-9)
     assert np.allclose(res[0].final_err[:M], ref.final_err[:M], rtol=1e-6, atol=0)
     assert np.allclose(np.concatenate(xs), ref.x, rtol=1e-9, atol=1e-12)
+    if N is not None:  # rank 0's cycle-1 residual against the reference's own run, not only HIP's
+        assert res[0].hist_res[0] == pytest.approx(_ref_cycle1(N, method), rel=1e-9)
 
 
 def _check_profile(outs, method):
@@ -143,7 +157,7 @@ def test_split_variant_in_process(N, variant, prod, R, method):
         assert not err, err
         assert all(o is not None for o in out)
         _check_profile([o[1] for o in out], method)
-        _compare(ref, [o[0] for o in out], [o[0].x for o in out])
+        _compare(ref, [o[0] for o in out], [o[0].x for o in out], N, method)
     finally:
         for c in ctxs:
             c.close()
@@ -274,6 +288,7 @@ def test_split_variant_processes_ipc(R, N, variant, prod, method):
     assert all(np.array_equal(vals[0][2], v[2]) and np.array_equal(vals[0][3], v[3]) for v in vals)
     assert vals[0][4] == M
     assert vals[0][2][0] == pytest.approx(ref.hist_res[0], rel=1e-9)
+    assert vals[0][2][0] == pytest.approx(_ref_cycle1(N, method), rel=1e-9)
     assert np.allclose(vals[0][3][:M], ref.final_err[:M], rtol=1e-6, atol=0)
     assert np.allclose(np.concatenate([v[5] for v in vals]), ref.x, rtol=1e-9, atol=1e-12)
     rt = vals[0][6]  # torch-free workers: the runtime the library links, not torch's bundled one

@@ -113,7 +113,12 @@ def test_build_refuses_chebyshev_scratch_spills():
                "gk_api.hip:9:1: remark: Function Name: _ZN2gk6k_projILi0ELb1ELi2EEEvPdPKdS3_\n"
                "gk_api.hip:9:1: remark:     ScratchSize [bytes/lane]: 32 [-Rpass-analysis=kernel-resource-usage]\n")
     assert b._scratch_kernels(remarks, "k_cheb_fused") == ["_ZN2gk12k_cheb_fusedILi8ELb1ELb1ELi1ELb0EEEvNS_6CFArgsE"]
-    assert [u[2] for u in b.HIP_UNITS] == ["gk_api.o"] + [f"gk_cheb{p}.o" for p in range(b.GK_CF_PARTS)]
+    assert [u[2] for u in b.HIP_UNITS] == (["gk_api.o"] + [f"gk_cheb{p}.o" for p in range(b.GK_CF_PARTS)]
+                                           + ["gk_blk.o"])
+    # the blocked-projection step's kernels (gk_blk.hip) are held to the same rule
+    rb = ("gk_blk.hip:46:1: remark: Function Name: _ZN2gk9k_mgs_blkILi32ELi0ELi2ELi9ELi2ELi4ELi0ELi512EEEvNS_7ResArgsE\n"
+          "gk_blk.hip:46:1: remark:     ScratchSize [bytes/lane]: 40 [-Rpass-analysis=kernel-resource-usage]\n")
+    assert b._scratch_kernels(rb, "k_mgs_blk") == ["_ZN2gk9k_mgs_blkILi32ELi0ELi2ELi9ELi2ELi4ELi0ELi512EEEvNS_7ResArgsE"]
 
 
 def test_torch_import_after_native_load_is_refused(built):

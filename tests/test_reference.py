@@ -28,7 +28,9 @@ KNOWN = json.load(open(os.path.join(HERE, "golden", "reference_known_answers.jso
 GMRES_SERIAL = sorted(k for k, v in REF.items()
                       if not k.startswith("_") and v["threads"] == 1 and not v["cut"]
                       and v["solver"] not in ("pcg_omp", "pbicgstab_omp"))
-KRYLOV = sorted(k for k, v in REF.items() if not k.startswith("_") and v["solver"] in ("pcg_omp", "pbicgstab_omp"))
+KRYLOV = sorted(k for k, v in REF.items()
+                if not k.startswith("_") and v["solver"] in ("pcg_omp", "pbicgstab_omp") and "hist_iter" not in v)
+KHIST = sorted(k for k, v in REF.items() if not k.startswith("_") and "hist_iter" in v)
 
 
 def _oracle_run(oracle, case, threads=1, max_cycles=1000):
@@ -68,6 +70,23 @@ def test_short_recurrence_oracle_vs_reference(oracle, key):
     assert it == g["iterations"]
     assert res == g["res"]
     assert np.array_equal(x, REFX[key])
+
+
+@pytest.mark.parametrize("key", KHIST)
+def test_short_recurrence_history_oracle_vs_reference(oracle, key):
+    """pcg_omp / pbicgstab_omp residual histories at 128^2 and 256^2 (round 5):
+    the reference records none, so tests/golden/make_ref_fixtures.py took it by
+    truncation -- the reference run from x0 = 0 with max_iter = k, one process
+    per k.  The restatement's per-iteration history equals it bit for bit, and so
+    do its iteration count and final residual."""
+    g = REF[key]
+    assert len(KHIST) == 8 and g["hist_iter"] == list(range(1, g["iterations"] + 1))
+    prec = {"identity": oracle.PREC_IDENTITY, "cbpr2": oracle.PREC_CBPR2}[g["prec"]]
+    fn = oracle.pcg if g["solver"] == "pcg_omp" else oracle.pbicgstab
+    x, it, res, hist = fn(oracle.rhs_ones(g["N"]), g["N"], 1e-9, g["m"], prec)
+    assert it == g["iterations"] and res == g["res"]
+    assert np.array_equal(np.asarray(hist[: len(g["hist_res"])]), np.array(g["hist_res"]))
+    assert [np.linalg.norm(x - 1.0), np.max(np.abs(x - 1.0))] == pytest.approx(g["x_err"], rel=1e-12)
 
 
 def test_oracle_1024_serial_three_cycles_bit_exact(oracle):

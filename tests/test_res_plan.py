@@ -62,5 +62,48 @@ def test_ranks_on_one_gpu_carry_the_production_load(N, prod, R):
 
 def test_query_rejects_bad_arguments():
     buf = (_native.c_ll * len(_native.RES_INFO_KEYS))()
-    assert _native.hip().gk_res_plan_query(1, 256, 1, 0, -1, buf) == -1
-    assert _native.hip().gk_res_plan_query(1 << 20, 0, 1, 0, -1, buf) == -1
+    assert _native.hip().gk_res_plan_query(1, 256, 1, 0, -1, 1, buf) == -1
+    assert _native.hip().gk_res_plan_query(1 << 20, 0, 1, 0, -1, 1, buf) == -1
+
+
+# The blocked-projection MGS step (GK_TUNE_RES_BLOCK = S, k_mgs_blk): the
+# instantiation every production split selects -- register chunks of w per
+# workgroup (512 threads; the w-only build 256 threads with LDS), the block cache
+# per slot (r2 registers / l2 LDS), the dynamic LDS that fits 160 KiB.
+BLOCKED = [
+    # N, ranks, S -> (wt, r2e, l2e, r2, l2)
+    (1024, 1, 2, (512, 4, 0, 4, 0)),
+    (4096, 8, 2, (512, 8, 0, 8, 0)),
+    (4096, 4, 2, (512, 16, 0, 7, 9)),
+    (4096, 2, 2, (512, 32, 0, 1, 9)),
+    (8192, 8, 2, (512, 32, 0, 1, 9)),
+    (4096, 1, 2, (256, 90, 38, 0, 0)),
+    (1024, 1, 4, (512, 4, 0, 4, 0)),
+    (4096, 8, 4, (512, 8, 0, 8, 0)),
+    (4096, 4, 4, (512, 16, 0, 2, 4)),
+    (4096, 2, 4, (512, 32, 0, 0, 4)),
+    (4096, 1, 4, (256, 88, 38, 0, 0)),
+]
+
+
+@pytest.mark.parametrize("N,R,S,want", BLOCKED)
+def test_blocked_plan_of_every_split(N, R, S, want):
+    nl = max(n for _, n in ga.slab_partition(N, R))
+    p = ga.res_plan_query(N * nl, 256, 1, False, -1, block=S)
+    assert p["variant"] == "blocked" and p["blk"] == S and p["G"] == 256, p
+    assert (p["wt"], p["r2e"], p["l2e"], p["r2"], p["l2"]) == want, p
+    lw = 38 if p["wt"] == 256 else 0
+    assert p["lds"] == (lw + S * p["l2"]) * p["wt"] * 16 and p["lds"] + 5 * 1024 <= 160 * 1024, p
+    # the whole slab is resident except the w-only S = 4 build's two streamed chunks
+    assert p["nres2"] <= N * nl // 2
+
+
+def test_blocked_plan_leaves_householder_strict():
+    for S in (2, 4):
+        p = ga.res_plan_query(4096 * 4096, 256, 1, True, -1, block=S)
+        assert p["variant"] != "blocked" and p["blk"] == 1, p
+
+
+def test_blocked_plan_rejects_other_blocks():
+    buf = (_native.c_ll * len(_native.RES_INFO_KEYS))()
+    assert _native.hip().gk_res_plan_query(1 << 20, 256, 1, 0, -1, 3, buf) == -1
