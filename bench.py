@@ -688,6 +688,29 @@ def config_legs(ga, prof_every: int) -> list[dict]:
 
 
 # ------------------------------------------------------------------- main ---
+def kfd_queues(pid: int | None = None):
+    """User-mode queues the KFD has created for this process (one per HIP hardware
+    queue in use: the context stream, the null stream, RCCL's, blit queues ...), from
+    /sys/class/kfd/kfd/proc/<pid>/queues; None where that is not readable."""
+    d = f"/sys/class/kfd/kfd/proc/{pid or os.getpid()}/queues"
+    try:
+        return len(os.listdir(d))
+    except OSError:
+        return None
+
+
+def kfd_sched_info() -> dict:
+    """The amdgpu scheduler limits that decide how many processes' queues the
+    hardware runs at once (readable module parameters only)."""
+    out = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}
+    for k in ("hws_max_conc_proc", "sched_policy", "mes", "cwsr_enable"):
+        try:
+            out[k] = open(f"/sys/module/amdgpu/parameters/{k}").read().strip()
+        except OSError:
+            pass
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -742,6 +765,8 @@ def main() -> None:
 
     ctl = Ctl(rank, world)  # out-of-band control plane (TCP on loopback); a no-op for one rank
     log("control plane up")
+    if rank == 0 and world > 1:
+        log(f"kfd scheduler: {kfd_sched_info()}")
 
     import gmres_amd as ga
 
@@ -778,7 +803,7 @@ def main() -> None:
     if world > 1 and args.collective in ("auto", "xgmi"):
         collective = setup_xgmi(ctx, ctl, rank,
                                 required=args.collective == "xgmi" or rccl_failed is not None) or "rccl"
-    log(f"collective: {collective or 'none'}")
+    log(f"collective: {collective or 'none'}; kfd user queues of this process: {kfd_queues()}")
     for kv in args.tune:
         k, v = kv.split("=")
         ctx.tune(int(k), int(v))
@@ -810,7 +835,7 @@ def main() -> None:
 
     fallback = None
     ok, why = guarded_warmup()
-    log(f"warmup {'done' if ok else 'FAILED'}")
+    log(f"warmup {'done' if ok else 'FAILED'}; kfd user queues of this process: {kfd_queues()}")
     if not ok:
         # Fallback, decided by all ranks together and REPORTED in the JSON line:
         # the launch-per-projection path, and RCCL instead of the device exchange

@@ -146,6 +146,7 @@ struct gk_ctx {
     int tune_res_wonly = -1;                        // large slabs: w-only variant (-1: by the byte model)
     int tune_verr_order = 1;                        // v_err diagnostics in the reference's dot order
     int tune_hh_fuse = 1;                           // Householder step: small launches folded into the chains
+    int tune_hh_norm_order = 0;                     // Householder: the reflector norms in flang-rt's order (1 rank)
     int res_share = 1;                              // contexts sharing this device's CUs
     int res_timeout_ms = 20000;
     bool res_broken = false;                        // a deadline was missed: launch path from then on
@@ -161,7 +162,6 @@ struct gk_ctx {
     int last_np = 0;          // partial count written by the last ACC-carrying sweep
     int tune_cheb_fused = 1;  // temporal-blocked Chebyshev sweeps (single slab)
     int tune_cheb_sten = 1;   // the Arnoldi step's pass forms z = A v itself (stage 0)
-    int tune_res_sten = 0;    // the w-only MGS step launch forms w = A V(:,j) itself (A/B: slower)
     int tune_spin_wait = 1;   // the per-step host wait spins on its event (0: hipEventSynchronize)
     int tune_graph = 1;       // launch-path MGS-R steps captured as hipGraphs (RCCL / no collective)
     int tune_res_qdef = -1;   // k_mgs_res NT: V_q of the LDS / streamed parts with the default policy (-1 auto)
@@ -176,7 +176,7 @@ struct gk_ctx {
     // tuning knobs (gk_set_tuning)
     int tune_nt = -1, tune_pj_blocks = 0, tune_st_blocks = 0;  // tune_nt: -1 auto
     bool nt_auto = false;
-    int tune_rev = 0, tune_blocked = 0, tune_unr = 0, proj_parity = 0;  // tune_unr 0 = auto
+    int tune_blocked = 0, tune_unr = 0;  // tune_unr 0 = auto
     int prof_every = 1;       // record events in steps with j % prof_every == 0
     bool prof_on_step = true;
     // state
@@ -620,66 +620,70 @@ int stencil(gk_ctx *c, int op, int acc, gk::StArgs a) {
 
 template <bool NT, int U>
 void launch_proj_u(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
-                   int npin, double *pout, double *hslot, double coef, i64 tail0, int rev, int hstore) {
+                   int npin, double *pout, double *hslot, double coef, i64 tail0, int hstore) {
     const dim3 g(c->np_pj);
     const i64 n = c->nloc;
     const int bl = c->tune_blocked;
     switch (mode) {
         case gk::PJ_DOT:
             gk::k_proj<gk::PJ_DOT, NT, U><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n,
-                                                                    tail0, rev, bl, hstore);
+                                                                    tail0, bl, hstore);
             break;
         case gk::PJ_AXPY:
             gk::k_proj<gk::PJ_AXPY, NT, U><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef, n,
-                                                                     tail0, rev, bl, hstore);
+                                                                     tail0, bl, hstore);
             break;
         case gk::PJ_AXPY_DOT:
             gk::k_proj<gk::PJ_AXPY_DOT, NT, U><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef,
-                                                                         n, tail0, rev, bl, hstore);
+                                                                         n, tail0, bl, hstore);
             break;
         default:
             gk::k_proj<gk::PJ_AXPY_NORM, NT, U><<<g, gk::TPB, 0, c->st>>>(w, va, vb, pin, npin, pout, hslot, coef,
-                                                                          n, tail0, rev, bl, hstore);
+                                                                          n, tail0, bl, hstore);
             break;
     }
 }
 
 template <bool NT>
 void launch_proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
-                 int npin, double *pout, double *hslot, double coef, i64 tail0, int rev, int hstore) {
+                 int npin, double *pout, double *hslot, double coef, i64 tail0, int hstore) {
     int u = c->tune_unr;
     if (u == 0) {  // auto: one trip per thread when the vector is small, else 2 in flight
         const i64 per_thread = (c->nloc / 2 + (i64)c->np_pj * gk::TPB - 1) / ((i64)c->np_pj * gk::TPB);
         u = per_thread <= 4 ? 4 : 2;
     }
     if (u == 2)
-        launch_proj_u<NT, 2>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
+        launch_proj_u<NT, 2>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, hstore);
     else if (u == 8)
-        launch_proj_u<NT, 8>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
+        launch_proj_u<NT, 8>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, hstore);
     else
-        launch_proj_u<NT, 4>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
+        launch_proj_u<NT, 4>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, hstore);
 }
 
 int proj(gk_ctx *c, int mode, double *w, const double *va, const double *vb, const double *pin,
          int npin, double *pout, double *hslot, double coef, i64 tail0 = 0, int hstore = 0) {
     ProfScope ps(c, GK_KID_PROJ);
-    int rev = 0;
-    if (c->tune_rev) {
-        c->proj_parity ^= 1;
-        rev = c->proj_parity;
-    }
     if (c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto))
-        launch_proj<true>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
+        launch_proj<true>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, hstore);
     else
-        launch_proj<false>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, rev, hstore);
+        launch_proj<false>(c, mode, w, va, vb, pin, npin, pout, hslot, coef, tail0, hstore);
     LAUNCHCHK();
     return GK_OK;
 }
 
 int scale(gk_ctx *c, double *out, const double *w, const double *pin, int npin, double *hslot,
-          double *hcopy = nullptr, const double *hsrc = nullptr, int ncopy = 0) {
+          double *hcopy = nullptr, const double *hsrc = nullptr, int ncopy = 0, bool pin_norm = false) {
     ProfScope ps(c, GK_KID_SCALE);
-    gk::k_scale<<<c->nblk_stream, gk::TPB, 0, c->st>>>(out, w, pin, npin, hslot, c->nloc, hcopy, hsrc, ncopy);
+    gk::k_scale<<<c->nblk_stream, gk::TPB, 0, c->st>>>(out, w, pin, npin, hslot, c->nloc, hcopy, hsrc, ncopy,
+                                                       pin_norm ? 1 : 0);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
+// NORM2 of x(0:n) in flang-rt's order into out[0] (GK_TUNE_HH_NORM_ORDER)
+int norm2_seq(gk_ctx *c, const double *x, i64 n, double *out) {
+    ProfScope ps(c, GK_KID_OTHER);
+    gk::k_norm2_seq<<<1, gk::TPB, 0, c->st>>>(x, n, out);
     LAUNCHCHK();
     return GK_OK;
 }
@@ -851,7 +855,7 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         spread(g.nt, g.rw, g.lw);
         p.r2 = g.rx;
         p.l2 = g.lx;
-        p.lds = (g.lw + tune_blk * g.lx) * g.nt * (int)sizeof(double2);
+        p.lds = (g.lw + tune_blk * (g.lx + g.pfx)) * g.nt * (int)sizeof(double2);
         p.nt = true;
         return;
     }
@@ -970,18 +974,18 @@ int launch_res_t(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     }
 }
 
-template <int MODE, bool STEN = false>
+template <int MODE>
 int launch_wres_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     constexpr int RW = MODE == gk::RES_MGS ? RES_RW : RES_RW_HH;
     constexpr int WBT = MODE == gk::RES_MGS ? gk::WB : gk::WB_HH;
     static std::atomic<int> attr[ATTR_DEVS];
     if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
     if (attr[c->dev].load() < p.lds) {
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RW, RES_LW, MODE, WBT, STEN>),
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RW, RES_LW, MODE, WBT>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
         attr[c->dev] = p.lds;
     }
-    gk::k_mgs_wres<RW, RES_LW, MODE, WBT, STEN><<<p.G, gk::WT, p.lds, c->st>>>(a);
+    gk::k_mgs_wres<RW, RES_LW, MODE, WBT><<<p.G, gk::WT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
 }
@@ -990,9 +994,7 @@ int launch_wres(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     switch (a.mode) {
         case gk::RES_HH_UP: return launch_wres_m<gk::RES_HH_UP>(c, p, a);
         case gk::RES_HH_DOWN: return launch_wres_m<gk::RES_HH_DOWN>(c, p, a);
-        default:
-            return a.sten_v != nullptr ? launch_wres_m<gk::RES_MGS, true>(c, p, a)
-                                       : launch_wres_m<gk::RES_MGS>(c, p, a);
+        default: return launch_wres_m<gk::RES_MGS>(c, p, a);
     }
 }
 
@@ -1060,22 +1062,16 @@ int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 //  flags (w-only variant, p.wo): RESF_CLOSE_HH -- RES_HH_UP also makes P(:,j+1) and
 //    writes w(1:j+1) to c->hb (one more exchange); RESF_UNIT_INIT -- RES_HH_DOWN builds
 //    its unit input e_{unit_g} itself.
-//  sten_v (RES_MGS, w-only variant): the launch forms w = A sten_v itself and the
-//    first dot with it (no pin); the halo lines of sten_v must be in c->hlo / c->hhi.
 enum { RESF_CLOSE_HH = 1, RESF_UNIT_INIT = 2, RESF_PIN_LOCAL = 4 };
 int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, double *hs, double *hcopy,
-             int mode = gk::RES_MGS, double *w = nullptr, i64 unit_g = -1, int flags = 0,
-             const double *sten_v = nullptr) {
+             int mode = gk::RES_MGS, double *w = nullptr, i64 unit_g = -1, int flags = 0) {
     ProfScope ps(c, GK_KID_RES);
     const bool close = (flags & RESF_CLOSE_HH) && mode == gk::RES_HH_UP;
     if ((flags & ~RESF_PIN_LOCAL) != 0 && !p.wo)
         return set_err(GK_ERR_STATE, "resident flags %d need the w-only variant", flags);
     const bool pin_local = (flags & RESF_PIN_LOCAL) && mode != gk::RES_HH_DOWN && c->xs_on && c->nranks > 1;
-    if (sten_v != nullptr && (!p.wo || mode != gk::RES_MGS || c->N % 2 != 0))
-        return set_err(GK_ERR_STATE, "the stencil prologue needs the w-only MGS step and even N");
-    // exchanges of the launch (the stencil prologue adds the first dot's)
-    const int np = (mode == gk::RES_MGS ? (p.blk > 1 ? gk::blk_exchanges(j, p.blk) : 2 * j) : j) + (close ? 1 : 0) +
-                   (sten_v != nullptr ? 1 : 0);
+    // exchanges of the launch
+    const int np = (mode == gk::RES_MGS ? (p.blk > 1 ? gk::blk_exchanges(j, p.blk) : 2 * j) : j) + (close ? 1 : 0);
     if (c->res_tag > 0xF0000000u) {  // tags must never repeat within the granule region's lifetime
         HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_ALL, c->st));
         c->res_tag = 1;
@@ -1114,14 +1110,9 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
         c->res_trace_g = p.G;
         c->res_trace_np = np;
     }
-    a.sten_v = sten_v;
     // auto: on -- A/B at 2896^2 (k_mgs_res<12, 18> NT, profiles/r04/ab_qdef_2896_r04a.jsonl): 19.98 /
     // 19.90 -> 18.82 / 18.84 us per projection
     a.qdef = c->tune_res_qdef != 0 ? 1 : 0;
-    a.slo = halo_lo(c);
-    a.shi = halo_hi(c);
-    a.N = c->N;
-    a.nlines = c->nlines;
     a.nranks = 1;
     if (c->xs_on && c->nranks > 1) {
         a.err = c->xs_err_dev;
@@ -1136,11 +1127,6 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
     return launch_res(c, p, a);
 }
 
-// Does the MGS step's resident launch form w = A V(:,j) itself (GK_TUNE_RES_STEN)?
-// The identity operator with the w-only variant and even N (double2 rows).
-bool res_sten(gk_ctx *c, const ResPlan &p) {
-    return c->tune_res_sten && p.wo && c->pkind == GK_PREC_IDENTITY && c->N % 2 == 0;
-}
 
 int d2h_sync(gk_ctx *c, double *host, const double *dev, int count) {
     HIPCHK(hipMemcpyAsync(c->hcol_host, dev, sizeof(double) * count, hipMemcpyDeviceToHost, c->st));
@@ -2178,14 +2164,6 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
     const int s0 = 0;
     ResPlan rp;
     const bool res = res_plan(c, rp);
-    if (res && res_sten(c, rp)) {  // w = A V(:,j), the first dot and the cascade: ONE launch
-        CHK(halo(c, V + (i64)(j - 1) * ld));
-        CHK(res_step(c, j, rp, nullptr, 0, hs, c->hallh_dev + (i64)(j - 1) * m2, gk::RES_MGS, nullptr, -1, 0,
-                     V + (i64)(j - 1) * ld));
-        HIPCHK(hipEventRecord(c->ev_step[j], c->st));
-        c->prof_on_step = true;
-        return GK_OK;
-    }
     // w = M^-1 A V(:,j), fused with the first dot <w, V(:,1)>
     CHK(op_precond(c, V + (i64)(j - 1) * ld, c->w, false, gk::ACC_DOT, V, slot(c, s0)));
     int np = c->last_np;
@@ -2202,7 +2180,7 @@ int gk_mgs_step_async(gk_ctx *c, int j) {
     }
     // Launch path: RCCL ranks (or one rank with the resident step off) replay the
     // step's projection chain as a hipGraph captured at its first use (GK_TUNE_GRAPH).
-    if (c->tune_graph && !c->tune_rev && (c->lg == nullptr || c->xs_on)) {
+    if (c->tune_graph && (c->lg == nullptr || c->xs_on)) {
         if (c->gkey != np) {
             graph_reset(c);
             c->gkey = np;
@@ -2302,6 +2280,10 @@ int gk_mgs_verr(gk_ctx *c, int n_out, int zero_last, double *v_err) {
 
 // ------------------------------------------------------------- Householder --
 
+// GK_TUNE_HH_NORM_ORDER: the reflector norms in flang-rt's order -- a running sum over
+// the whole vector, so one rank only (N ranks keep the tree).
+static bool hh_seq_norms(const gk_ctx *c) { return c->tune_hh_norm_order != 0 && c->nranks == 1; }
+
 static int hh_pivot(gk_ctx *c, int j, double *hostout, int nout) {
     // hb[0..j] = w(1:j+1) from the owning rank, broadcast
     const int root = owner_of(c, j);
@@ -2330,17 +2312,27 @@ int gk_hh_cycle_start(gk_ctx *c, int precondition, double *g1) {
         CHK(stencil(c, gk::OP_RESID, gk::ACC_NORM, a));
     }
     CHK(allreduce(c, slot(c, 0), c->last_np));
+    // GK_TUNE_HH_NORM_ORDER: beta = norm2(w) and norm2 of the fixed w in the reference's
+    // order (gmres_hh.f90:250-253), one rank
+    const bool seq = hh_seq_norms(c);
+    if (seq) CHK(norm2_seq(c, c->w, c->nloc, slot(c, 0)));
     CHK(hh_pivot(c, 0, nullptr, 0));
     {
         ProfScope ps(c, GK_KID_OTHER);
-        gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, 0), c->last_np, 0, c->hcol, c->scal + 2);
+        gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, 0), seq ? 1 : c->last_np, 0, c->hcol, c->scal + 2,
+                                                 nullptr, seq ? 1 : 0);
         LAUNCHCHK();
         // w(1) = sign(beta,w(1)) + w(1); norm2(w)
         gk::k_hh_fix<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->w, c->nloc, c->g0, 0, 0, c->scal + 2, slot(c, 1));
         LAUNCHCHK();
     }
-    CHK(allreduce(c, slot(c, 1), c->nblk_stream));
-    CHK(scale(c, c->V, c->w, slot(c, 1), c->nblk_stream, nullptr));
+    if (seq) {
+        CHK(norm2_seq(c, c->w, c->nloc, slot(c, 1)));
+        CHK(scale(c, c->V, c->w, slot(c, 1), 1, nullptr, nullptr, nullptr, 0, true));
+    } else {
+        CHK(allreduce(c, slot(c, 1), c->nblk_stream));
+        CHK(scale(c, c->V, c->w, slot(c, 1), c->nblk_stream, nullptr));
+    }
     CHK(d2h_sync(c, g1, c->hcol, 1));
     c->cycle_hh = true;
     c->cycle_mgs = false;
@@ -2359,7 +2351,8 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
     // chain ends with the fix-up and P(:,j+1) = w/||w|| (no k_hh_fix, no k_scale).
     ResPlan rp;
     const bool res = res_plan(c, rp, true);
-    const bool fuse = res && rp.wo && c->tune_hh_fuse != 0;
+    const bool seq = hh_seq_norms(c);  // reference-order reflector norms: the unfused step
+    const bool fuse = res && rp.wo && c->tune_hh_fuse != 0 && !seq;
     // v_j = e_j ; v_j = P_1 .. P_j e_j
     if (!fuse) {
         ProfScope ps(c, GK_KID_OTHER);
@@ -2422,18 +2415,27 @@ int gk_hh_step_async(gk_ctx *c, int j, int precondition) {
         }
         CHK(allreduce(c, slot(c, s0), np));
     }
+    if (seq) {  // tmp = norm2(w(j+1:n)) in the reference's order (gmres_hh.f90:307)
+        CHK(norm2_seq(c, c->w + j, c->nloc - j, slot(c, s0)));
+        np = 1;
+    }
     CHK(hh_pivot(c, j, nullptr, 0));
     {
         ProfScope ps(c, GK_KID_OTHER);
         const int m2 = c->m + 2;
         gk::k_hh_pivot<<<1, gk::TPB, 0, c->st>>>(c->hb, slot(c, s0), np, j, c->hall + (i64)(j - 1) * m2,
-                                                 c->scal + 2, c->hallh_dev + (i64)(j - 1) * m2);
+                                                 c->scal + 2, c->hallh_dev + (i64)(j - 1) * m2, seq ? 1 : 0);
         LAUNCHCHK();
         gk::k_hh_fix<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->w, c->nloc, c->g0, j, j, c->scal + 2, slot(c, s1));
         LAUNCHCHK();
     }
-    CHK(allreduce(c, slot(c, s1), c->nblk_stream));
-    CHK(scale(c, P + (i64)j * ld, c->w, slot(c, s1), c->nblk_stream, nullptr));
+    if (seq) {  // w = w / norm2(w) (gmres_hh.f90:315)
+        CHK(norm2_seq(c, c->w, c->nloc, slot(c, s1)));
+        CHK(scale(c, P + (i64)j * ld, c->w, slot(c, s1), 1, nullptr, nullptr, nullptr, 0, true));
+    } else {
+        CHK(allreduce(c, slot(c, s1), c->nblk_stream));
+        CHK(scale(c, P + (i64)j * ld, c->w, slot(c, s1), c->nblk_stream, nullptr));
+    }
     HIPCHK(hipEventRecord(c->ev_step[j], c->st));
     return GK_OK;
 }
@@ -2540,7 +2542,9 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_PROJ_NT: c->tune_nt = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_PROJ_BLOCKS: c->tune_pj_blocks = value; break;
         case GK_TUNE_STENCIL_BLOCKS: c->tune_st_blocks = value; break;
-        case GK_TUNE_PROJ_REV: c->tune_rev = value != 0; break;
+        case GK_TUNE_PROJ_REV:  // removed in round 5 (measured no gain)
+            if (value != 0) return set_err(GK_ERR_ARG, "GK_TUNE_PROJ_REV was removed (the reversed launch-path walk)");
+            break;
         case GK_TUNE_CHEB_FUSED: c->tune_cheb_fused = value != 0; break;
         case GK_TUNE_PROJ_BLOCKED: c->tune_blocked = value != 0; break;
         case GK_TUNE_XCHG_TIMEOUT_MS:
@@ -2561,13 +2565,17 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_RES_WONLY: c->tune_res_wonly = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_HH_FUSE: c->tune_hh_fuse = value != 0; break;
         case GK_TUNE_CHEB_STEN: c->tune_cheb_sten = value != 0; break;
-        case GK_TUNE_RES_STEN: c->tune_res_sten = value != 0; break;
+        case GK_TUNE_RES_STEN:  // removed in round 5: measured 4 % slower (profiles/r03/ab_res_sten_r03k.jsonl)
+            if (value != 0) return set_err(GK_ERR_ARG, "GK_TUNE_RES_STEN was removed (the stencil prologue of the "
+                                                       "w-only step measured 4 %% slower)");
+            break;
         case GK_TUNE_SPIN_WAIT: c->tune_spin_wait = value != 0; break;
         case GK_TUNE_GRAPH: c->tune_graph = value != 0; break;
         case GK_TUNE_RES_QDEF: c->tune_res_qdef = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_RES_PC: c->tune_res_pc = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_RES_FOLD: c->tune_res_fold = value != 0; break;
         case GK_TUNE_WATCHDOG_MS: c->watchdog_ms = std::max(0, value); break;
+        case GK_TUNE_HH_NORM_ORDER: c->tune_hh_norm_order = value != 0; break;
         case GK_TUNE_RES_BLOCK:
             if (value != 1 && value != 2 && value != 4)
                 return set_err(GK_ERR_ARG, "GK_TUNE_RES_BLOCK %d: blocks of 1 (strict MGS-R), 2 or 4 projections", value);
@@ -2766,7 +2774,7 @@ int gk_res_info(gk_ctx *c, int hh, long long *info) {
     ResPlan p;
     const bool on = res_plan(c, p, hh != 0);
     plan_info(p, on, info);
-    info[RPI_STEN] = on && hh == 0 && res_sten(c, p) ? 1 : 0;
+    info[RPI_STEN] = 0;  // the step launch never forms w = A V(:,j) itself (GK_TUNE_RES_STEN removed)
     // op_precond_sten's conditions, without its collective (the smallest slab of
     // a multi-rank context is gathered at its first solve)
     int cs = c->pkind == GK_PREC_CHEB && c->tune_cheb_sten && c->pdeg <= gk::CF_LMAX && c->N >= gk::CF_PTS &&

@@ -61,15 +61,22 @@ constexpr int BLK_WB_LDS = GK_BLK_WB_LDS;
 // caches: no extra HBM bytes), so the unrolled pass has no per-column branches.
 // TCH > 0: the waves not busy with the all-gather touch the first TCH chunks of
 // the following pass's last dot column into L2 (k_mgs_wres's paced touch).
+// PFX > 0 (small slabs, whose pass is one memory latency): the dot block of the
+// NEXT pass is loaded for chunks 0 .. PFX-1 straight into LDS (global_load_lds,
+// no VGPRs) before each all-gather, so its loads overlap the all-gather instead of
+// opening the next pass (the strict small-slab kernel's prefetch, k_mgs_res PF).
 // --------------------------------------------------------------------------
-template <int RW, int LW, int RX, int LX, int S, int WBT, int TCH, int NT>
+typedef __attribute__((address_space(3))) void lds_void_t;
+template <int RW, int LW, int RX, int LX, int S, int WBT, int TCH, int NT, int PFX = 0>
 __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     static_assert(S >= 2 && S <= RES_SMAX, "blocks of 2..RES_SMAX projections");
     static_assert(RX + LX <= RW, "the column cache covers register chunks of w only");
+    static_assert(PFX <= RX && (PFX == 0 || (LW == 0 && LX == 0)), "the prefetch covers register-cached chunks");
     constexpr int NW = NT / 64, KM = 2 * S - 1;
     extern __shared__ double2 lsh[];
     double2 *__restrict__ lw = lsh;            // [LW][NT]: w beyond the registers
     double2 *__restrict__ lx = lsh + LW * NT;  // [S][LX][NT]: cached columns, chunks RX .. RX+LX-1
+    double2 *__restrict__ lpf = lx + S * LX * NT;  // [S][PFX][NT]: the next pass's dot block (PFX > 0)
     __shared__ double sm[KM][NW];
     __shared__ double bc[KM];
     __shared__ double hv[S];      // h of the block the next pass subtracts, by slot (0: dummy)
@@ -100,6 +107,24 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     auto at = [&](const double2 *base, int c) {  // element t of chunk c of a column
         return reinterpret_cast<const double2 *>(reinterpret_cast<const char *>(base + (i64)c * NT) + vo);
     };
+    // the dot block (id, rd) of the next pass, chunks < PFX, into lpf by global_load_lds
+    // (dummy slots load the block's first real column: finite values for h = 0)
+    auto prefetch = [&](int id, int rd) {
+        if constexpr (PFX > 0) {
+            int cb, ce;
+            range(cb, ce);
+#pragma unroll
+            for (int d = 0; d < S; ++d) {
+                const int qd = d - (S - rd);
+                const double2 *D = V2 + (i64)(id + (qd > 0 ? qd : 0)) * ld2;
+#pragma unroll
+                for (int k = 0; k < PFX; ++k)
+                    if (cb + k < ce)
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(at(D, cb + k)),
+                                                         (lds_void_t *)(lpf + (d * PFX + k) * NT + (t & ~63)), 16, 0, 0);
+            }
+        }
+    };
     double2 wr[RW], xc[S][RX > 0 ? RX : 1];
     // w, and V(:,1) -- block 0, subtracted by pass 0 from slot S-1 -- into the cache
     // (the dummy slots zero)
@@ -122,10 +147,12 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     }
     for (int k = 0; k < LW; ++k)
         if (l0 + k < lend) lw[k * NT + t] = W2[(l0 + k) * NT + t];
+    prefetch(blk_lo(1 % nb1, S), blk_n(1 % nb1, S, j));  // pass 0's dot block
     // h of block 0 = <w, V(:,1)>: the operator launch's partial slab (on N ranks
     // its rank hop here, res_pin_fold)
     double h;
     {
+        if constexpr (PFX > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         double s = 0.0;
         for (int k = t; k < a.npin; k += NT) s += a.pin[k];
         s = wave_sum(s);
@@ -189,8 +216,12 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
                 const int k = k0 + u;
                 if (k < RW && cb + k < ce) {
 #pragma unroll
-                    for (int d = 0; d < S; ++d)
-                        bv[u][d] = k < RX + LX ? ldv<true>(at(D[d], cb + k)) : ldv<false>(at(D[d], cb + k));
+                    for (int d = 0; d < S; ++d) {
+                        if (k < PFX)  // (the norm pass reads a stale but finite block here: unused)
+                            bv[u][d] = lpf[(d * PFX + (k < PFX ? k : 0)) * NT + t];
+                        else
+                            bv[u][d] = k < RX + LX ? ldv<true>(at(D[d], cb + k)) : ldv<false>(at(D[d], cb + k));
+                    }
                     if (k >= RX + LX) {
 #pragma unroll
                         for (int s = 0; s < S; ++s) av[u][s] = ldv<true>(at(A[s], cb + k));
@@ -321,6 +352,10 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
             xdone = 0;
         }
         __syncthreads();
+        if (p + 2 < P) {  // the next pass reduces dots: its block's loads overlap this all-gather
+            const int b2 = (p + 2) % nb1;
+            prefetch(blk_lo(b2, S), blk_n(b2, S, j));
+        }
         // value v on wave v (and v + NW, ... when a block has more values than waves)
         for (int v = wv; v < (KM <= NW ? (wv < K ? wv + 1 : 0) : K); v += NW) {
             double s = sm[v][0];
@@ -350,6 +385,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
                 }
             }
         }
+        if constexpr (PFX > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
         __syncthreads();
         if constexpr (TCH > 0) asm volatile("s_waitcnt vmcnt(0)" : : "v"(touch_sink) : "memory");
         ++xi;
@@ -423,14 +459,14 @@ struct BlkCfg;
 // deeper batch or more cached register chunks spilled)
 template <>
 struct BlkCfg<2> {
-    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512}, {8, 0, 8, 0, 512}, {16, 0, 7, 9, 512},
-                                            {32, 0, 1, 9, 512}, {90, 38, 0, 0, 256}};
+    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4}, {8, 0, 8, 0, 512, 8}, {16, 0, 7, 9, 512, 0},
+                                            {32, 0, 1, 9, 512, 0}, {90, 38, 0, 0, 256, 0}};
     static constexpr int wb[BLK_NVAR] = {4, 4, 4, 2, 4};
 };
 template <>
 struct BlkCfg<4> {
-    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512}, {8, 0, 8, 0, 512}, {16, 0, 2, 4, 512},
-                                            {32, 0, 0, 4, 512}, {88, 38, 0, 0, 256}};
+    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4}, {8, 0, 8, 0, 512, 2}, {16, 0, 2, 4, 512, 0},
+                                            {32, 0, 0, 4, 512, 0}, {88, 38, 0, 0, 256, 0}};
     static constexpr int wb[BLK_NVAR] = {4, 2, 2, 1, 2};
 };
 
@@ -439,7 +475,7 @@ int launch_v(const ResArgs &a, int G, int lds, int dev, hipStream_t st) {
     constexpr BlkGeom g = BlkCfg<S>::g[V];
     constexpr int WBT = BlkCfg<S>::wb[V];
     constexpr int TCH = V == BLK_WONLY ? BLK_TOUCH : 0;
-    auto kern = &k_mgs_blk<g.rw, g.lw, g.rx, g.lx, S, WBT, TCH, g.nt>;
+    auto kern = &k_mgs_blk<g.rw, g.lw, g.rx, g.lx, S, WBT, TCH, g.nt, g.pfx>;
     static std::atomic<int> attr[64];
     if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
     if (lds > 0 && attr[dev].load() < lds) {
@@ -467,7 +503,7 @@ int launch_s(int var, const ResArgs &a, int G, int lds, int dev, hipStream_t st)
 }  // namespace
 
 BlkGeom blk_geom(int var, int S) {
-    if (var < 0 || var >= BLK_NVAR) return BlkGeom{0, 0, 0, 0, 0};
+    if (var < 0 || var >= BLK_NVAR) return BlkGeom{0, 0, 0, 0, 0, 0};
     return S == 4 ? BlkCfg<4>::g[var] : BlkCfg<2>::g[var];
 }
 

@@ -36,6 +36,7 @@ __host__ __device__ constexpr int blk_exchanges(int j, int S) { return 2 * blk_s
 enum { BLK_R4 = 0, BLK_R8 = 1, BLK_R16 = 2, BLK_R32 = 3, BLK_WONLY = 4, BLK_NVAR = 5 };
 struct BlkGeom {
     int rw, lw, rx, lx, nt;  // w chunks in registers / LDS, cached column chunks in registers / LDS, threads
+    int pfx;                 // chunks of the next pass's dot block prefetched into LDS (small slabs)
 };
 BlkGeom blk_geom(int var, int S);
 int blk_variant(long long chunks512);  // chunks per thread at 512 threads; BLK_WONLY past 32

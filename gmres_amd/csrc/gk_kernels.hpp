@@ -43,7 +43,7 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
                                               const double *__restrict__ vb,
                                               const double *__restrict__ pin, int npin,
                                               double *__restrict__ pout, double *__restrict__ hslot,
-                                              double coef, i64 n, i64 tail0, int rev, int blocked,
+                                              double coef, i64 n, i64 tail0, int blocked,
                                               int hstore) {
     __shared__ double sm[WAVES];
     const i64 n2 = n >> 1;
@@ -51,9 +51,7 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
     const double2 *__restrict__ A2 = reinterpret_cast<const double2 *>(va);
     const double2 *__restrict__ B2 = reinterpret_cast<const double2 *>(vb);
     // Work mapping: grid-stride over U*TPB double2 chunks (default), or one
-    // contiguous range per workgroup (blocked); rev walks the vector from the
-    // top so the lines the previous launch touched last are reused first
-    // from the Infinity Cache.
+    // contiguous range per workgroup (blocked).
     i64 lo, hi, step;
     if (blocked) {
         const i64 chunk = (i64)TPB * U;
@@ -72,7 +70,7 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const i64 e = base + (i64)u * TPB;
-            idx[u] = (e < hi) ? (rev ? n2 - 1 - e : e) : -1;
+            idx[u] = (e < hi) ? e : -1;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -141,13 +139,15 @@ __global__ __launch_bounds__(TPB) void k_proj(double *__restrict__ w, const doub
 // of the reference's Inf/NaN.
 // hcopy (optional): block 0 also publishes hsrc[0..ncopy) and h to hcopy
 // (mapped pinned host memory: the step's Hessenberg column, no extra copy).
+// pin_norm: pin[0] is h itself (a norm taken in the reference's order, k_norm2_seq).
 __global__ __launch_bounds__(TPB) void k_scale(double *__restrict__ out, const double *__restrict__ w,
                                                const double *__restrict__ pin, int npin,
                                                double *__restrict__ hslot, i64 n,
                                                double *__restrict__ hcopy = nullptr,
-                                               const double *__restrict__ hsrc = nullptr, int ncopy = 0) {
+                                               const double *__restrict__ hsrc = nullptr, int ncopy = 0,
+                                               int pin_norm = 0) {
     __shared__ double sm[WAVES];
-    const double h = sqrt(reduce_slab(pin, npin, sm));
+    const double h = pin_norm ? pin[0] : sqrt(reduce_slab(pin, npin, sm));
     if (hslot != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hslot = h;
     if (hcopy != nullptr && blockIdx.x == 0) {
         for (int k = threadIdx.x; k < ncopy; k += TPB) hcopy[k] = hsrc[k];
@@ -169,6 +169,41 @@ __global__ __launch_bounds__(TPB) void k_scale(double *__restrict__ out, const d
         for (i64 e = (i64)blockIdx.x * TPB + threadIdx.x; e < n2; e += stride) O2[e] = double2{0.0, 0.0};
         if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) out[n - 1] = 0.0;
     }
+}
+
+// out[0] = NORM2(x(0:n)) as flang-rt computes it (Norm2Accumulator<8>: a running
+// max m and a scaled sum s, result m sqrt(1 + s); oracle/gmres_oracle.c or_norm2) --
+// the reference's serial norm2 of gmres_hh.f90:251-253,307,315, in its order.  One
+// workgroup: chunks of TPB elements staged through LDS, thread 0 folds each in order
+// (GK_TUNE_HH_NORM_ORDER, single rank; ~2 us per 256 elements).
+__global__ __launch_bounds__(TPB) void k_norm2_seq(const double *__restrict__ x, i64 n, double *__restrict__ out) {
+    __shared__ double buf[TPB];
+    double mx = 0.0, s = 0.0;
+    for (i64 c0 = 0; c0 < n; c0 += TPB) {
+        const i64 e = c0 + threadIdx.x;
+        buf[threadIdx.x] = e < n ? x[e] : 0.0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int cnt = n - c0 < TPB ? (int)(n - c0) : TPB;
+            for (int k = 0; k < cnt; ++k) {
+                const double a = fabs(buf[k]);
+                if (mx == 0.0) {
+                    mx = a;
+                } else if (a > mx) {
+                    const double t = mx / a;
+                    const double tsq = t * t;
+                    s = s * tsq;
+                    s = s + tsq;
+                    mx = a;
+                } else {
+                    const double t = a / mx;
+                    s = s + t * t;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = mx * sqrt(1.0 + s);
 }
 
 // out[0] = sqrt(sum(pin)) or sum(pin).
@@ -307,11 +342,12 @@ __global__ __launch_bounds__(TPB) void k_hh_fix(double *__restrict__ w, i64 n, i
 //                  -> res[0] = g1, delta[0] = sign(beta, w1)          (:250-252)
 //  step  (j >= 1): tmp = sqrt(tail); H(j+1,j) = w(j+1) > 0 ? -tmp : tmp
 //                  -> hcol[0..j-1] = w(1:j), hcol[j] = H(j+1,j), delta = -H (:306-316)
+// pin_norm: pin[0] is the norm itself (k_norm2_seq) instead of a partial slab of squares.
 __global__ void k_hh_pivot(const double *__restrict__ hb, const double *__restrict__ pin, int npin,
                            int j, double *__restrict__ hcol, double *__restrict__ delta,
-                           double *__restrict__ hcopy = nullptr) {
+                           double *__restrict__ hcopy = nullptr, int pin_norm = 0) {
     __shared__ double sm[WAVES];
-    const double s = sqrt(reduce_slab(pin, npin, sm));
+    const double s = pin_norm ? pin[0] : sqrt(reduce_slab(pin, npin, sm));
     if (j == 0) {
         if (threadIdx.x == 0) {
             const double w1 = hb[0];
@@ -843,7 +879,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         __syncthreads();
-        if (t < 64) res_exchange<RWAVES, CW, MODE == RES_MGS, RES_POLL_SLEEP_SMALL>(a, xi, sm, bc, &okf);
+        if (t < 64) res_exchange<RWAVES, MODE == RES_MGS, RES_POLL_SLEEP_SMALL>(a, xi, sm, bc, &okf);
         __syncthreads();
         ++xi;
         h = bc[0];
@@ -974,7 +1010,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                     if (c0 + k < cend) X[k] = ldv<NT>(colchunk(q2, c0 + k) + td);
             }
         }
-        if (t < 64) res_exchange<RWAVES, CW, MODE == RES_MGS, RES_POLL_SLEEP_SMALL>(a, xi, sm, bc, &okf);
+        if (t < 64) res_exchange<RWAVES, MODE == RES_MGS, RES_POLL_SLEEP_SMALL>(a, xi, sm, bc, &okf);
         __syncthreads();
         ++xi;
         h = bc[0];
@@ -1053,20 +1089,18 @@ constexpr int WT = 256;  // threads per workgroup (4 waves, one per SIMD)
 #ifndef GK_RES_WB
 #define GK_RES_WB 8
 #endif
-#ifndef GK_RES_XPF
-#define GK_RES_XPF 0
-#endif
 constexpr int WB = GK_RES_WB;        // double2 per column per batch in flight per thread
 #ifndef GK_RES_WB_HH
 #define GK_RES_WB_HH 6
 #endif
 constexpr int WB_HH = GK_RES_WB_HH;  // the reflection chains' batch (their RW is larger)
-// XPF 1: every wave loads the next pass's first batch before the exchange wait;
-// 2: waves 1..3 only (wave 0 runs the exchange: its polls would queue behind
-// its own prefetch loads, vmcnt retiring in issue order).  Measured: 1 is
-// slower (42.4 -> 46.9 us per projection at RW 80), so the default is 0.
-constexpr int XPF_MODE = GK_RES_XPF;
-constexpr bool XPF = XPF_MODE != 0;
+// (Round 5 removed measured-slower A/B paths from this kernel: XPF -- the next
+// pass's first batch loaded before the exchange wait, 42.4 -> 46.9 us per projection
+// at RW 80; ROT -- every workgroup's chunk range moved to its neighbour's, the even
+// XCDs lagged as before (profiles/r02/res_trace_rotation.jsonl); REV -- the LDS part
+// walked in alternating halves, 40.89 -> 44.05 us (profiles/r04/ab_rev_wb_r04i.jsonl);
+// STEN -- the stencil formed in the prologue, 245.9 -> 236.2 it/s
+// (profiles/r03/ab_res_sten_r03k.jsonl).  DESIGN.md 3.1 keeps the numbers.)
 // TOUCH: while wave 0 runs a pass's all-gather, waves 1..3 pull the first
 // TOUCH chunks (4 KiB each) of the NEXT pass's dot column -- the one that
 // comes from HBM -- into L2 with one dword load per 128-B line into a sink
@@ -1088,10 +1122,6 @@ constexpr int TOUCH = GK_RES_TOUCH;
 // 16 / 20 / 24 / 28 / 32 / 40 / 48 -> 41.47 / 41.08 / 41.04 / 40.78 / 41.17 / 42.7 / 43.6
 // us per projection (two boxes); Householder 24 vs 32: 40.76 vs 41.96 us per reflection.
 constexpr int TOUCH_MGS = GK_RES_TOUCH_MGS;
-#ifndef GK_RES_ROT
-#define GK_RES_ROT 0
-#endif
-constexpr int RES_ROT = GK_RES_ROT;
 // Load policy of the dot column V_q of a pass (A/B knob): 0 = default, so the
 // column is still in the Infinity Cache when the next pass reads it as its
 // AXPY column V_i; 1 = non-temporal like V_i (every column comes from HBM).
@@ -1119,26 +1149,9 @@ constexpr int TOUCH_PACE = GK_RES_TOUCH_PACE;
 // the reflection chains' pacing (0 = burst); re-measured after the depth / residency
 // re-tune (profiles/r02/ab_pace_retune.jsonl): 8 / 24 -> 41.06 / 41.1 vs 40.57 us burst
 constexpr int TOUCH_PACE_HH = GK_RES_TOUCH_PACE_HH;
-#ifndef GK_RES_REV
-#define GK_RES_REV 0
-#endif
-// REV (A/B knob): the LDS part of a workgroup's chunks is split into halves lo /
-// hi; even passes walk lo, registers, hi and odd passes hi, registers, lo, so a
-// pass's AXPY column V_i -- the previous pass's dot column -- starts with the
-// half that pass read last, on lines still in L2 (a half: 19 chunks of 4 KiB
-// per column, inside a workgroup's 128 KiB share of its XCD's L2).  The register
-// part keeps one order (a second unrolled order spills).  The touch of the next
-// dot column covers the half the next pass starts with.
-constexpr bool RES_REV = GK_RES_REV != 0;
 
-// STEN (RES_MGS, identity operator): the launch forms w = A V(:,j) in its
-// prologue -- the stencil launch's arithmetic, ((W+E)+N)+S and 4x - s, element
-// by element from V(:,j) and its halo lines -- and takes the first dot
-// <w, V(:,1)> with it as one more in-launch all-gather, instead of reading w
-// and the partial slab of a separate stencil launch (gmres_mgsr.f90:336,346).
-template <int RW, int LW, int MODE, int WBT = WB, bool STEN = false>
+template <int RW, int LW, int MODE, int WBT = WB>
 __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
-    static_assert(!STEN || MODE == RES_MGS, "the stencil prologue is the MGS step's");
     extern __shared__ double2 lw[];  // [LW][WT]
     __shared__ double sm[WT / 64];
     __shared__ double bc[1];
@@ -1152,9 +1165,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     const int j = a.j, np = res_np(mode, j);
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
     const i64 nch = a.nres2 / WT;
-    // chunk range of this workgroup: that of workgroup (b + ROT) mod G (ROT != 0: an A/B
-    // knob that moves the data relative to the XCDs)
-    const i64 bq = ((i64)blockIdx.x + RES_ROT) % gridDim.x;
+    const i64 bq = blockIdx.x;  // chunk range of this workgroup
     const i64 c0 = bq * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
     const i64 l0 = (i64)gridDim.x * a.r2e + bq * a.l2e, lend = l0 + a.l2e < nch ? l0 + a.l2e : nch;
     const i64 tail0 = mode == RES_HH_UP ? a.tail0 : 0;
@@ -1177,67 +1188,11 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             if (l0 + k < lend) lw[k * WT + t] = unit2((l0 + k) * WT + t);
         for (i64 e = sbase; e < n2; e += sstride) W2[e] = unit2(e);
         if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.w[a.n - 1] = (a.n - 1 == u) ? 1.0 : 0.0;
-    } else if (!STEN) {
+    } else {
 #pragma unroll
         for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
         for (int k = 0; k < LW; ++k)
             if (l0 + k < lend) lw[k * WT + t] = W2[(l0 + k) * WT + t];
-    }
-    // STEN: w = A V(:,j) at double2 index e2 (local elements 2 e2, 2 e2 + 1; N even)
-    // and the first dot's partial <w, V(:,1)>, batches of SB chunks in flight
-    double sten_acc = 0.0;
-    if constexpr (STEN) {
-        const double *__restrict__ vj = a.sten_v;
-        const double2 *__restrict__ Vj2 = reinterpret_cast<const double2 *>(vj);
-        const double2 *__restrict__ Lo2 = reinterpret_cast<const double2 *>(a.slo);
-        const double2 *__restrict__ Hi2 = reinterpret_cast<const double2 *>(a.shi);
-        const int N = a.N, hN = a.N >> 1, nl = a.nlines;
-        struct Ld {
-            double2 c, up, dn, v1;
-            double l, r;
-        };
-        auto load = [&](i64 e2) {
-            Ld q;
-            const int g = (int)(2 * e2), row = g / N, col = g - row * N;
-            q.c = Vj2[e2];
-            q.l = col > 0 ? vj[g - 1] : 0.0;
-            q.r = col + 2 < N ? vj[g + 2] : 0.0;
-            q.up = row + 1 < nl ? Vj2[e2 + hN] : (Hi2 != nullptr ? Hi2[col >> 1] : double2{0.0, 0.0});
-            q.dn = row > 0 ? Vj2[e2 - hN] : (Lo2 != nullptr ? Lo2[col >> 1] : double2{0.0, 0.0});
-            q.v1 = V2[e2];
-            return q;
-        };
-        auto make = [&](const Ld &q) {
-            const double s0 = ((q.l + q.c.y) + q.up.x) + q.dn.x;
-            const double s1 = ((q.c.x + q.r) + q.up.y) + q.dn.y;
-            const double2 w2 = double2{4.0 * q.c.x - 1.0 * s0, 4.0 * q.c.y - 1.0 * s1};
-            sten_acc = sten_acc + w2.x * q.v1.x;
-            sten_acc = sten_acc + w2.y * q.v1.y;
-            return w2;
-        };
-        constexpr int SB = 4;
-#pragma unroll
-        for (int k0 = 0; k0 < RW; k0 += SB) {
-            Ld q[SB];
-#pragma unroll
-            for (int u = 0; u < SB; ++u)
-                if (k0 + u < RW && c0 + k0 + u < cend) q[u] = load((c0 + k0 + u) * WT + t);
-#pragma unroll
-            for (int u = 0; u < SB; ++u) {
-                const int k = k0 + u;
-                if (k < RW) wr[k] = (c0 + k < cend) ? make(q[u]) : double2{0.0, 0.0};
-            }
-        }
-        for (int k0 = 0; k0 < LW; k0 += SB) {
-            Ld q[SB];
-#pragma unroll
-            for (int u = 0; u < SB; ++u)
-                if (k0 + u < LW && l0 + k0 + u < lend) q[u] = load((l0 + k0 + u) * WT + t);
-#pragma unroll
-            for (int u = 0; u < SB; ++u)
-                if (k0 + u < LW && l0 + k0 + u < lend) lw[(k0 + u) * WT + t] = make(q[u]);
-        }
-        for (i64 e = sbase; e < n2; e += sstride) W2[e] = make(load(e));  // streamed part: to HBM
     }
     // acc += the closing reduction of element pair e2 (local double2 index)
     auto red = [&](double &acc, const double2 &v, const double2 &b, int kind, i64 e2, bool chk) {
@@ -1248,27 +1203,9 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             sq_acc(acc, v, e2, tail0, chk);
         }
     };
-    // XPF: the first batch of a pass (its two columns are known before the dot
-    // that scales it) is loaded before the previous pass's exchange wait, so the
-    // memory pipe is busy while the all-gather completes.
-    double2 pa[WBT], pb[WBT];
-    const bool xpf_wave = XPF_MODE == 1 || (XPF_MODE == 2 && t >= 64);
-    auto load_first = [&](int i, int q, bool dot) {
-        if (!xpf_wave) return;
-        const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
-        const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
-#pragma unroll
-        for (int u = 0; u < WBT; ++u) {
-            const i64 c = c0 + u;
-            if (u < RW && c < cend) {
-                pa[u] = ldv<true>(A2 + c * WT + t);
-                if (dot) pb[u] = ldv<RES_QNT>(B2 + c * WT + t);
-            }
-        }
-    };
     // One pass over the slab: w -= ch V_i, then the reduction `kind`
     // (<w, V_q>, ||w(tail0:)||^2, or none).  Returns this thread's partial.
-    auto pass = [&](double ch, int i, int q, int kind, bool rev) -> double {
+    auto pass = [&](double ch, int i, int q, int kind) -> double {
         const double2 *__restrict__ A2 = V2 + (i64)i * ld2;
         const double2 *__restrict__ B2 = V2 + (i64)q * ld2;
         const bool dot = kind == RK_DOT;
@@ -1279,10 +1216,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
 #pragma unroll
             for (int u = 0; u < WBT; ++u) {
                 const i64 c = c0 + k0 + u;
-                if (XPF && k0 == 0 && xpf_wave && !rev) {
-                    av[u] = pa[u];
-                    bv[u] = pb[u];
-                } else if (k0 + u < RW && c < cend) {
+                if (k0 + u < RW && c < cend) {
                     av[u] = ldv<true>(A2 + c * WT + t);
                     if (dot) bv[u] = ldv<RES_QNT>(B2 + c * WT + t);
                 }
@@ -1320,13 +1254,9 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 }
             }
         };
-        constexpr int LH = RES_REV ? LW / 2 : 0;  // LDS halves [0, LH) and [LH, LW)
-        const int f0 = rev ? LH : 0, f1 = rev ? LW : LH;  // the half walked first
-        for (int k0 = f0; k0 < f1; k0 += WBT) lbatch(k0, f1);
 #pragma unroll
         for (int k0 = 0; k0 < RW; k0 += WBT) rbatch(k0);
-        const int s0 = rev ? 0 : LH, s1 = rev ? LH : LW;  // and last
-        for (int k0 = s0; k0 < s1; k0 += WBT) lbatch(k0, s1);
+        for (int k0 = 0; k0 < LW; k0 += WBT) lbatch(k0, LW);
         for (i64 e0 = sbase; e0 < n2; e0 += 2 * sstride) {  // streamed part: 32 B/unknown
             double2 wv[2], av[2], bv[2];
 #pragma unroll
@@ -1360,26 +1290,21 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     };
     // all-gather of the partials: the same h in every workgroup (and rank)
     int xi = 0;
-    auto reduce = [&](double acc, double &h, int touch_col, bool trev = false) -> bool {
+    auto reduce = [&](double acc, double &h, int touch_col) -> bool {
         clk.passed(a.stamps);
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
         if (PACE > 0 && t == 0) xdone = 0;
         __syncthreads();
         if (t < 64) {
-            res_exchange<WT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
+            res_exchange<WT / 64, MODE == RES_MGS, RES_POLL_SLEEP>(a, xi, sm, bc, &okf);
             if (PACE > 0 && t == 0) *(volatile int *)&xdone = 1;
         } else if constexpr (TCH > 0) {
             if (touch_col >= 0) {
                 // lines [0, 32*TCH) of the workgroup's register-resident part of
                 // the column (contiguous from chunk c0); all loads land in one sink
                 // register, drained below before anything can reuse it
-                // (REV: the LDS half the next pass starts with)
-                i64 r0 = c0, r1 = cend;
-                if constexpr (RES_REV) {
-                    r0 = trev ? l0 + LW / 2 : l0;
-                    r1 = trev ? lend : (l0 + LW / 2 < lend ? l0 + LW / 2 : lend);
-                }
+                const i64 r0 = c0, r1 = cend;
                 const i64 lines = (i64)32 * (r1 - r0 < TCH ? (r1 - r0 > 0 ? r1 - r0 : 0) : TCH);
                 const char *base = reinterpret_cast<const char *>(V2 + (i64)touch_col * ld2 + r0 * WT);
                 for (i64 l = t - 64; l < lines; l += WT - 64) {
@@ -1404,27 +1329,20 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     // back from, so the pass code of all three modes is the same (the tail test
     // inside the unrolled loop made the UP pass 28 % slower: 45.9 vs 35.7 us).
     auto kind_of = [&](int p) { return p < np - 1 ? RK_DOT : (mode == RES_MGS ? RK_NORM : RK_NONE); };
-    auto rev_of = [&](int p) { return RES_REV && (p & 1) != 0; };
     double h;
     bool ok = true;
     if (mode == RES_HH_DOWN) {
         // the pre-dot as an AXPY pass with h = 0 (w - 0 V = w): a dot-only copy of the
         // unrolled register loop would not fit the register file
         const int q = res_col(mode, j, 0);
-        if (XPF) load_first(q, q, true);
         double acc = 0.0;
         if (a.unit_known) {  // <e_u, P_q> = P_q(u): the one nonzero product, as the full sum gives it
             if (blockIdx.x == 0 && t == 0 && a.unit_e >= 0) acc = a.V[(i64)q * a.ld + a.unit_e];
         } else {
-            acc = pass(0.0, q, q, RK_DOT, false);
+            acc = pass(0.0, q, q, RK_DOT);
         }
-        if (XPF) load_first(q, res_col(mode, j, 1), kind_of(0) == RK_DOT);
         ok = reduce(acc, h, kind_of(0) == RK_DOT ? res_col(mode, j, 1) : -1);
-    } else if constexpr (STEN) {
-        if (XPF) load_first(res_col(mode, j, 0), res_col(mode, j, 1), kind_of(0) == RK_DOT);
-        ok = reduce(sten_acc, h, kind_of(0) == RK_DOT ? res_col(mode, j, 1) : -1);
     } else {
-        if (XPF) load_first(res_col(mode, j, 0), res_col(mode, j, 1), kind_of(0) == RK_DOT);
         double s = 0.0;
         for (int k = t; k < a.npin; k += WT) s += a.pin[k];
         s = wave_sum(s);
@@ -1440,11 +1358,9 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         const int i = res_col(mode, j, p);
         const int kind = kind_of(p);
         if (mode == RES_MGS && blockIdx.x == 0 && t == 0) hsh[i] = (p < j ? 0.0 : hsh[i]) + h;  // H(i,j) (+)= h
-        const double acc = pass(mode == RES_MGS ? h : a.coef * h, i, res_col(mode, j, p + 1), kind, rev_of(p));
-        if (XPF && p + 1 < np && !rev_of(p + 1))
-            load_first(res_col(mode, j, p + 1), res_col(mode, j, p + 2), kind_of(p + 1) == RK_DOT);
+        const double acc = pass(mode == RES_MGS ? h : a.coef * h, i, res_col(mode, j, p + 1), kind);
         if (kind != RK_NONE)
-            ok = reduce(acc, h, p + 1 < np && kind_of(p + 1) == RK_DOT ? res_col(mode, j, p + 2) : -1, rev_of(p + 1));
+            ok = reduce(acc, h, p + 1 < np && kind_of(p + 1) == RK_DOT ? res_col(mode, j, p + 2) : -1);
     }
     if (!ok) return;  // uniform per workgroup; *err is set
     const bool close = mode == RES_HH_UP && a.close_hh;
@@ -1709,7 +1625,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_wpc(ResArgs a) {
         if (t == 0) xdone = 0;
         __syncthreads();
         if (t < 64) {
-            res_exchange<NT / 64, false, MODE == RES_MGS, RES_POLL_SLEEP_PC>(a, xi, sm, bc, &okf);
+            res_exchange<NT / 64, MODE == RES_MGS, RES_POLL_SLEEP_PC>(a, xi, sm, bc, &okf);
             if (t == 0) *(volatile int *)&xdone = 1;
         } else if constexpr (TCHP > 0) {
             if (touch_col >= 0) {

@@ -135,10 +135,6 @@ struct ResArgs {
     double *hb;           // close_hh: w(1:j+1) before the fix-up, written by the owner rank (pivot input)
     int unit_init;        // RES_HH_DOWN with unit_known: the launch builds e_u itself (w not read)
     u64 *trace;           // gk_profile_res_trace (nullptr = off): [workgroup][RES_TRACE_X][publish, seen] ticks
-    // w-only kernel, RES_MGS with STEN: the launch forms w = A V(:,j) itself
-    const double *sten_v;         // V(:,j)
-    const double *slo, *shi;      // its halo lines -1 / nlines (nullptr: the physical boundary)
-    int N, nlines;                // grid side, slab lines
     // k_mgs_res with NT: the LDS-held and streamed parts load their dot column V_q
     // with the default policy (it is the next pass's AXPY column V_i: then an
     // Infinity-Cache hit), V_i non-temporal -- the w-only kernel's policy
@@ -234,18 +230,12 @@ __device__ __forceinline__ double block_sum_rt(double v, double *sm) {
 // G partials of the grid (8 granules in flight per lane) and sum them in a
 // fixed order; on N ranks then add the rank totals in rank order.  Result in
 // bc[0]; *okf = 0 when a deadline passed (then *err is set).
-#ifndef GK_RES_XHOPS
-#define GK_RES_XHOPS 1
-#endif
-// 1: every workgroup sweeps all partials; 2: via group leaders, in the
-// small-grid kernel (k_mgs_res with a control wave) only.  A/B with one granule
-// array (profiles/r02/ab_hops_*.jsonl): two hops 4.25 vs 4.37 us per projection at
-// 1024^2 (256 readers of one array congested the flat sweep), but 10.9 vs 10.4 at
-// 2048^2 and 43.2 vs 41.6 at 4096^2.  With 8 replicas (RES_NREP) the flat sweep
-// wins at 1024^2 too: 3.85 vs 4.1 us (profiles/r02/ab_nrep_1024.jsonl).
-constexpr int RES_XHOPS = GK_RES_XHOPS;
-constexpr int RES_NG = 8;                     // groups of the two-hop all-gather (blockIdx % 8)
-constexpr int RES_MK = (2 * RGMAX / RES_NG + 63) / 64;  // granule loads per lane of a leader's sweep
+// (Round 5: the two-hop all-gather -- 8 group leaders summing their members and
+// publishing group sums, GK_RES_XHOPS 2 -- was removed from the kernels.  It won at
+// 1024^2 only while one granule array was swept by all 256 workgroups, 4.25 vs 4.37
+// us per projection (profiles/r02/ab_hops_*.jsonl); with the replicas below the flat
+// sweep is faster there too, 3.88 vs 4.1 us (profiles/r02/ab_nrep_1024.jsonl), and it
+// always was at 2048^2 (10.4 vs 10.9) and 4096^2 (41.6 vs 43.2).)
 #ifndef GK_RES_NREP
 #define GK_RES_NREP 8
 #endif
@@ -258,8 +248,8 @@ constexpr int RES_MK = (2 * RGMAX / RES_NG + 63) / 64;  // granule loads per lan
 // top of the array size, so they fall on different channels).  1 = one array.
 constexpr int RES_NREP = GK_RES_NREP;
 constexpr i64 RES_REP_STRIDE = 4 * (i64)RGMAX + 32;
-constexpr i64 RES_REP0 = 4 * (i64)RGMAX + 4 * RES_NG;  // first replica (RES_NREP > 1)
-// [2][RGMAX][2] partials + [2][NG][2] group sums + the replicas
+constexpr i64 RES_REP0 = 4 * (i64)RGMAX + 32;  // first replica (RES_NREP > 1)
+// [2][RGMAX][2] partials + 32 words (once the two-hop group sums) + the replicas
 constexpr i64 RES_GATH_WORDS = RES_REP0 + (RES_NREP > 1 ? RES_NREP * RES_REP_STRIDE : 0);
 // rank totals of the resident launches: replica r in value slot XS_REP_STEP * r (128 B apart)
 constexpr int XS_REP_STEP = 8;
@@ -286,12 +276,11 @@ constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
 // completes, polls its granules without the sleep (its detection delay is on
 // every rank's critical path; the other workgroups' is not).
 constexpr bool RES_PUSHER_FAST = GK_RES_PUSHER_FAST != 0;
-#ifndef GK_RES_SWEEP_ALL
-#define GK_RES_SWEEP_ALL 0
-#endif
-// N ranks: 1 = every workgroup sweeps the local granules (the earlier protocol),
-// 0 = only workgroup 0 does (A/B knob).  The totals are the same bits either way.
-constexpr bool RES_SWEEP_ALL = GK_RES_SWEEP_ALL != 0;
+// N ranks: only workgroup 0 sweeps the local granules (every workgroup reads the R
+// rank totals, its own rank's among them).  Round 5 removed the A/B knob that let
+// every workgroup sweep (GK_RES_SWEEP_ALL): the same bits, a tie in the same-device
+// rehearsals (profiles/r04/ab_sweep_r04x.jsonl: 605 / 601, 1,094 / 1,093, 1,546 /
+// 1,529 it/s pusher-only / all).
 constexpr int RES_POLL_SLEEP_SMALL = GK_RES_POLL_SLEEP_SMALL;
 #ifndef GK_RES_POLL_SLEEP_PC
 #define GK_RES_POLL_SLEEP_PC 16
@@ -359,7 +348,7 @@ __device__ __forceinline__ bool res_pin_fold(const ResArgs &a, double &h, double
 
 // TR: the trace stamps (gk_profile_res_trace) are compiled into the MGS-R launches only
 // (the reflection kernels are at the edge of the register file).
-template <int NW = RWAVES, bool HOP2 = false, bool TR = false, int SLEEP = RES_POLL_SLEEP>
+template <int NW = RWAVES, bool TR = false, int SLEEP = RES_POLL_SLEEP>
 __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const double *sm, double *bc, int *okf) {
     const int lane = threadIdx.x;
     const int G = gridDim.x;
@@ -383,90 +372,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
     const u64 deadline = wall_clock64() + a.timeout;
     double acc = 0.0;
     bool all_ok = true;
-    if (HOP2 && RES_XHOPS == 2 && G > 2 * RES_NG) {
-        // Two hops.  Hop 1: the leader of group g (workgroup g < RES_NG) sweeps
-        // the granules of its members g, g + NG, g + 2NG, ... (under round-robin
-        // dispatch one XCD's workgroups: same-XCD traffic, never assumed for
-        // correctness) and publishes their sum, in member order, as a granule
-        // pair.  Hop 2: every workgroup reads the NG group sums and adds them in
-        // group order.  256 readers of 16 granules instead of 256 readers of
-        // 2G: the sweep load that queued at the granules' memory channel.
-        u64 *gs = a.gath + 4 * (i64)RGMAX + (i64)(p & 1) * RES_NG * 2;
-        if ((int)blockIdx.x < RES_NG) {
-            const int g = blockIdx.x;
-            const int nmem = (G - 1 - g) / RES_NG + 1;  // members of group g
-            unsigned v[RES_MK];
-            for (;;) {
-                u64 x[RES_MK];
-#pragma unroll
-                for (int k = 0; k < RES_MK; ++k) {  // granule gi = lane + 64k of the group: member gi/2, half gi&1
-                    const int gi = lane + 64 * k, b = g + RES_NG * (gi >> 1);
-                    x[k] = __hip_atomic_load(slot + (gi < 2 * nmem ? 2 * b + (gi & 1) : 0), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-                }
-                bool ok = true;
-#pragma unroll
-                for (int k = 0; k < RES_MK; ++k) {
-                    const bool in = lane + 64 * k < 2 * nmem;
-                    v[k] = in ? (unsigned)x[k] : 0u;
-                    ok = ok && (!in || (unsigned)(x[k] >> 32) == tag);
-                }
-                if (__all(ok)) break;
-                if (wall_clock64() > deadline) {
-                    all_ok = false;
-                    int miss = 0x7FFF;
-#pragma unroll
-                    for (int k = 0; k < RES_MK; ++k) {
-                        const int gi = lane + 64 * k;
-                        if (gi < 2 * nmem && (unsigned)(x[k] >> 32) != tag) miss = min(miss, g + RES_NG * (gi >> 1));
-                    }
-                    for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, 64));
-                    if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(SLEEP);
-            }
-            double gsum = 0.0;
-#pragma unroll
-            for (int k = 0; k < RES_MK; ++k) {  // members in increasing order per lane pair
-                const unsigned o = __shfl_xor(v[k], 1, 64);
-                const unsigned lo = (lane & 1) ? o : v[k], hi = (lane & 1) ? v[k] : o;
-                if (!(lane & 1) && lane + 64 * k < 2 * nmem)
-                    gsum = gsum + __longlong_as_double((long long)(((u64)hi << 32) | lo));
-            }
-            gsum = wave_sum(gsum);
-            if (lane < 2 && all_ok) {
-                const u64 bits = (u64)__double_as_longlong(gsum);
-                __hip_atomic_store(gs + 2 * g + lane, ((u64)tag << 32) | (lane ? (unsigned)(bits >> 32) : (unsigned)bits),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        // hop 2: lanes 0 .. 2NG-1 hold the halves of the group sums
-        unsigned d = 0;
-        while (all_ok) {
-            const u64 x = __hip_atomic_load(gs + (lane < 2 * RES_NG ? lane : 0), __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-            const bool ok = lane >= 2 * RES_NG || (unsigned)(x >> 32) == tag;
-            d = (unsigned)x;
-            if (__all(ok)) break;
-            if (wall_clock64() > deadline) {
-                all_ok = false;
-                int miss = ok ? 0x7FFF : (lane >> 1);
-                for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, 64));
-                if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);  // the leader of the missing group
-                break;
-            }
-            __builtin_amdgcn_s_sleep(SLEEP);
-        }
-        double r = 0.0;
-#pragma unroll
-        for (int q = 0; q < RES_NG; ++q) {  // group order, the same instructions in every workgroup
-            const unsigned lo = __builtin_amdgcn_readlane(d, 2 * q), hi = __builtin_amdgcn_readlane(d, 2 * q + 1);
-            const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
-            r = (q == 0) ? v : r + v;
-        }
-        acc = all_ok ? r : 0.0;
-    } else if (RES_SWEEP_ALL || a.nranks == 1 || blockIdx.x == 0) {
+    if (a.nranks == 1 || blockIdx.x == 0) {
         // (N ranks: only workgroup 0, the pusher, needs this rank's total -- every
         // workgroup then reads the R rank totals, its own rank's included, so the
         // others skip the sweep and its polls stay off the stragglers' memory path.)

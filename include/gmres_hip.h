@@ -319,8 +319,8 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          non-temporal when a vector exceeds 48 MiB)
  *   GK_TUNE_PROJ_BLOCKS    workgroups of the projection kernel (0 = auto)
  *   GK_TUNE_STENCIL_BLOCKS target workgroups of the stencil sweeps (0 = auto)
- *   GK_TUNE_PROJ_REV       1: alternate the traversal direction of successive
- *                          projection launches (Infinity Cache reuse)
+ *   GK_TUNE_PROJ_REV       removed in round 5 (1 is refused): the alternating traversal of
+ *                          successive projection launches
  *   GK_TUNE_PROJ_BLOCKED   1: contiguous range per workgroup; 0: grid-stride
  *   GK_TUNE_PROJ_UNROLL    double2 loads in flight per thread and array: 2, 4, 8; 0 = auto
  *   GK_TUNE_CHEB_FUSED     1 (default): Chebyshev(k <= 8) as temporal-blocked passes of up to
@@ -355,11 +355,8 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *   GK_TUNE_CHEB_STEN      1 (default): the Arnoldi step's Chebyshev(k <= 8) pass forms z = A v
  *                          itself in a stage ahead of its levels (no stencil launch, no z vector;
  *                          N >= 128, slabs of at least k + 1 lines); 0: stencil launch + pass
- *   GK_TUNE_RES_STEN       0 (default): stencil launch + resident step; 1: with the identity
- *                          operator the w-only resident MGS step forms w = A V(:,j) in its prologue
- *                          and takes the first dot with it (no stencil launch; even N) -- measured
- *                          4 % slower at 4096^2: the prologue's loads cannot be kept in flight beside
- *                          the register-resident w
+ *   GK_TUNE_RES_STEN       removed in round 5 (1 is refused): the w-only step forming w = A V(:,j)
+ *                          in its prologue measured 4 % slower at 4096^2
  *   GK_TUNE_GRAPH          1 (default): a launch-path MGS-R step (RCCL ranks, device-exchange ranks
  *                          with the resident step off, or one rank with it off) is captured once
  *                          per step index j as a hipGraph -- its 2j projection launches, 2j + 1
@@ -398,6 +395,13 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          kernel of the context was never scheduled) and the context is
  *                          BROKEN: every later call returns GK_ERR_STATE; gk_destroy frees it
  *                          once its stream drains (bounded by the same limit; else it is kept)
+ *   GK_TUNE_HH_NORM_ORDER  0 (default): the Householder reflector norms (gmres_hh.f90:251-253,
+ *                          307, 315) tree-reduced in the resident chains; 1 (one rank): taken
+ *                          in the reference's own order -- flang-rt's NORM2, a running max and
+ *                          scaled sum over the vector (k_norm2_seq) -- so the device basis
+ *                          carries the reference's normalisation rounding (the v_err band of
+ *                          DESIGN.md 4.3 becomes two-sided); the step runs unfused.  A
+ *                          diagnostic mode: one sequential pass per norm (~0.1 ms per 16 K)
  *   GK_TUNE_SPIN_WAIT      1 (default): gk_mgs_step_wait / gk_hh_step_wait spin on the step's
  *                          event; 0: hipEventSynchronize (may sleep in the driver per step) */
 #define GK_TUNE_PROJ_NT 0
@@ -425,6 +429,7 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_RES_FOLD 22
 #define GK_TUNE_RES_BLOCK 23
 #define GK_TUNE_WATCHDOG_MS 24
+#define GK_TUNE_HH_NORM_ORDER 25
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 /* Test hook: hold = 1 enqueues on the context's stream a wait for a mapped host
  * word that only hold = 0 writes (hipStreamWaitValue32) -- every later kernel of

@@ -185,28 +185,3 @@ def test_fused_stencil_stage_matches_stencil_launch(N, degree):
     for a, b in zip(res[1][0], res[0][0]):
         assert np.allclose(a, b, rtol=1e-12, atol=1e-15)
     assert np.allclose(res[1][1], res[0][1], rtol=1e-10, atol=1e-14)
-
-
-def test_resident_stencil_prologue_matches_stencil_launch():
-    """GK_TUNE_RES_STEN (an A/B knob, off by default: measured slower): the
-    w-only resident MGS step forming w = A V(:,j) in its prologue (and the
-    first dot with it) against the stencil launch + resident step, at 4096^2
-    (the w-only variant's grid): the same element arithmetic, so the
-    Hessenberg columns of steps 1..4 and V(:,5) agree up to the dots'
-    summation order."""
-    import gmres_amd as ga
-    from gmres_amd import _native as nat
-
-    N = 4096
-    res = {}
-    for sten in (1, 0):
-        with ga.Context(N, 10) as c:
-            c.tune(nat.GK_TUNE_RES_STEN, sten)
-            c.set_precond("identity", (8.2, 0.2), 1)
-            c.set_rhs_ones()
-            c.mgs_cycle_start()
-            cols = [c.mgs_step(j) for j in range(1, 5)]
-            res[sten] = (cols, _ctx_col(c, 4))
-    for a, b in zip(res[1][0], res[0][0]):
-        assert np.allclose(a, b, rtol=1e-12, atol=1e-15)
-    assert np.allclose(res[1][1], res[0][1], rtol=1e-10, atol=1e-14)

@@ -274,6 +274,33 @@ def test_hh_verr_vs_reference_run(oracle):
     _hh_verr_close(r.v_err[1:30], ref["v_err"][1:30], below=1.5)
 
 
+def test_hh_verr_two_sided_with_reference_order_norms(oracle):
+    """with the reflector norms taken in the reference's own
+    order (GK_TUNE_HH_NORM_ORDER: flang-rt's NORM2 running max + scaled sum,
+    gmres_hh.f90:251-253,307,315) the device basis carries the reference's
+    normalisation rounding, and its calculate_verr after the 128^2 m=30 run to
+    convergence falls inside the TWO-sided band of the reference's own figure
+    (the default tree-reduced norms sit 1.08 decades below it:
+    test_hh_verr_vs_reference_run).  (a) by value as always: the device figure
+    equals the reference's formula on the device basis."""
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+    from tests import verr_host as vh
+
+    ref = json.load(open(os.path.join(HERE, "golden", "reference_runs.json")))["hh_omp_identity_128_m30"]
+    with ga.Context(128, 30) as ctx:
+        ctx.tune(nat.GK_TUNE_HH_NORM_ORDER, 1)
+        ctx.set_rhs_ones()
+        r = ga.gmres_hh(ctx, 1e-15, precondition=False, max_cycles=1000)
+        P = [ctx.get_basis(k, 0) for k in range(r.n_out)]
+    assert r.n_out == ref["n_out"] == 30 and abs(r.iterations - ref["iterations"]) <= 0.01 * ref["iterations"]
+    assert np.array_equal(r.v_err[1:30], vh.hh_verr(P, 30, vh.ref_dot(oracle))[1:30])
+    d = np.log10(np.sum(r.v_err[1:30]) / np.sum(ref["v_err"][1:30]))
+    print(f"\n[hh norm order] v_err sum vs reference: {d:+.2f} decades; median entry "
+          f"{np.median(np.log10(np.asarray(r.v_err[1:30]) / np.asarray(ref['v_err'][1:30]))):+.2f}")
+    _hh_verr_close(r.v_err[1:30], ref["v_err"][1:30])  # two-sided: +-0.7 decades, median |d| <= 0.8
+
+
 def test_true_residual_and_solution(oracle):
     import gmres_amd as ga
 
@@ -408,7 +435,11 @@ def test_short_recurrence_history_vs_reference(solver, prec, N):
         assert np.all(dev <= rt), np.nonzero(dev > rt)[0][:10]
     else:
         assert abs(it - it_ref) <= max(3, 0.15 * it_ref), (it, it_ref)
-        early = r > 1e-1 * r[0]
+        # the first decade: the iterations BEFORE the residual first drops below r0 / 10
+        # (BiCGSTAB's residual is not monotone: a late spike above r0 / 10 is no longer
+        # comparable between reduction orders)
+        k10 = int(np.argmax(r <= 1e-1 * r[0])) if np.any(r <= 1e-1 * r[0]) else len(r)
+        early = np.arange(len(r)) < k10
         dev = np.abs(h[early] - r[early]) / r[early]
         print(f"\n[{solver} {prec} {N}^2] {it} vs {it_ref} iterations; max rel dev over the first decade: "
               f"{dev.max():.2e}")
