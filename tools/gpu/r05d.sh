@@ -24,3 +24,15 @@ print(sys.argv[2], "S", sys.argv[3], "it/s", round(d["value"], 1), "frac", d["ro
 PY
   done
 done
+# 4096^2: the Infinity-Cache policy of the blocked w-only build's second dot slot
+for v in base q1c0 q1c64 q1c90; do
+  if [ $v = base ]; then unset GK_LIB_DIR; else export GK_LIB_DIR=$PWD/gmres_amd/lib/variants/$v; fi
+  timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --grid 4096 --no-cpu --no-configs \
+    --tune 23=2 > $out/bench_4096_s2_$v.json 2> $out/bench_4096_s2_$v.err || exit $?
+  python - "$out/bench_4096_s2_$v.json" "$v" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+sp = d.get("diagnostics", {}).get("resident_split_per_unit_us", {}).get("mgs_step", {})
+print("4096 S 2", sys.argv[2], "it/s", round(d["value"], 1), "frac", d["roofline"].get("frac"), "split", sp)
+PY
+done
