@@ -1634,10 +1634,10 @@ int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out)
         hipHostGetDevicePointer((void **)&c->hallh_dev, c->hallh, 0) != hipSuccess)
         return fail(set_err(GK_ERR_NOMEM, "cannot allocate the Hessenberg mirrors"));
     if (hipMalloc(&c->res_gath, sizeof(gk::u64) * gk::RES_GATH_ALL) != hipSuccess ||
-        hipMalloc(&c->res_gm, sizeof(double) * (size_t)(m + 1) * gk::RES_SMAX) != hipSuccess ||
+        hipMalloc(&c->res_gm, sizeof(double) * (size_t)(m + 1 + gk::RES_SMAX) * gk::RES_SMAX) != hipSuccess ||
         hipHostMalloc((void **)&c->res_err, sizeof(int), hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void **)&c->res_err_dev, c->res_err, 0) != hipSuccess ||
-        hipMemsetAsync(c->res_gm, 0, sizeof(double) * (size_t)(m + 1) * gk::RES_SMAX, c->st) != hipSuccess ||
+        hipMemsetAsync(c->res_gm, 0, sizeof(double) * (size_t)(m + 1 + gk::RES_SMAX) * gk::RES_SMAX, c->st) != hipSuccess ||
         hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_ALL, c->st) != hipSuccess)
         return fail(set_err(GK_ERR_NOMEM, "cannot allocate the resident-step exchange area"));
     *c->res_err = 0;

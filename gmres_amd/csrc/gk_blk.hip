@@ -36,6 +36,11 @@ constexpr int BLK_POLL_SLEEP = GK_BLK_POLL_SLEEP;
 // batch of the LDS part of w (its loop is not unrolled: a deeper batch spilled the
 // one-wave build, whose registers hold 88 chunks of w)
 constexpr int BLK_WB_LDS = GK_BLK_WB_LDS;
+// Dot columns not cached on chip are read with the default policy: they come back
+// as the next pass's AXPY columns.  (At 4096^2 the S dot columns of a pass outgrow
+// the 256 MiB Infinity Cache; reading the second slot non-temporal -- wholly, past
+// chunk 64 or past the 90 register chunks -- measured slower still: 196.4 / 196.1 /
+// 202.1 vs 210.6 it/s, profiles/r05/ab_blk_qdef_4096_r05d.txt.)
 
 }  // namespace
 
@@ -49,8 +54,8 @@ constexpr int BLK_WB_LDS = GK_BLK_WB_LDS;
 // past the cache the AXPY columns are read again, the dot columns then with the
 // default policy so that re-read is an Infinity-Cache hit), subtracts the current
 // block's columns with the h it holds, takes the dots and the Gram terms with the
-// block's last column, and closes with ONE multi-value all-gather (res_exchange_v:
-// value v on wave v).  Thread 0 then forms the next block's h by the recurrence of
+// block's last column, and closes with ONE multi-value all-gather (res_publish_v /
+// res_collect_v: value v on wave v).  Thread 0 then forms the next block's h by the recurrence of
 // gk_blk.hpp.  The last pass closes with ||w||^2; V(:,j+1) = w / ||w|| and
 // H(1:j+1, j) as in the strict kernels.
 //
@@ -80,7 +85,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     __shared__ double sm[KM][NW];
     __shared__ double bc[KM];
     __shared__ double hv[S];      // h of the block the next pass subtracts, by slot (0: dummy)
-    __shared__ double gsh[RES_SMAX * RES_SMAX];  // stored Gram terms of the block the pass dots with
+    __shared__ double gbuf[(RES_SMAX - 1) * RES_SMAX];  // Gram table rows of the block a pass dots with
     __shared__ int okf, xdone;
     __shared__ double hsh[RHMAX + 1];
     const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
@@ -219,8 +224,10 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
                     for (int d = 0; d < S; ++d) {
                         if (k < PFX)  // (the norm pass reads a stale but finite block here: unused)
                             bv[u][d] = lpf[(d * PFX + (k < PFX ? k : 0)) * NT + t];
+                        else if (k < RX + LX)
+                            bv[u][d] = ldv<true>(at(D[d], cb + k));
                         else
-                            bv[u][d] = k < RX + LX ? ldv<true>(at(D[d], cb + k)) : ldv<false>(at(D[d], cb + k));
+                            bv[u][d] = ldv<false>(at(D[d], cb + k));
                     }
                     if (k >= RX + LX) {
 #pragma unroll
@@ -266,7 +273,8 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
                 const i64 c = l0 + k0 + u;
                 if (k0 + u < LW && c < lend) {
 #pragma unroll
-                    for (int d = 0; d < S; ++d) bv[u][d] = ldv<false>(at(D[d], (int)c));
+                    for (int d = 0; d < S; ++d)
+                        bv[u][d] = ldv<false>(at(D[d], (int)c));
 #pragma unroll
                     for (int s = 0; s < S; ++s) av[u][s] = ldv<true>(at(A[s], (int)c));
                 }
@@ -321,13 +329,12 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
         const int bd = (p + 1) % nb1, id = blk_lo(bd, S), rd = last ? 1 : blk_n(bd, S, j);
         const bool gram = !last && bd == nb1 - 1 && rd >= 2;  // the block of the newest column j-1
         // the stored Gram terms of block bd (the newest column's come with this
-        // all-gather), loaded by thread 0 -- their only reader -- while the pass streams:
-        // gsh[k * S + l] = <V(id+l), V(id+k)>, l < k < rd
-        if (t == 0 && !last) {
-            for (int k = 1; k < rd; ++k)
-                if (!(gram && k == rd - 1))
-                    for (int l = 0; l < k; ++l) gsh[k * S + l] = a.gm[(i64)(id + k) * RES_SMAX + (k - l)];
-        }
+        // all-gather): rows id+1 .. id+S-1 of the table, straight into LDS by wave 0
+        // (global_load_lds: no VGPRs, no wait) for thread 0's recurrence after the
+        // all-gather -- gbuf[(k-1) * RES_SMAX + d] = <V(id+k-d), V(id+k)>
+        if (!last && t < 2 * (S - 1))
+            __builtin_amdgcn_global_load_lds(
+                reinterpret_cast<const void *>(a.gm + (i64)(id + 1) * RES_SMAX + 2 * t), (lds_void_t *)gbuf, 16, 0, 0);
         pass(last, ia, ra, id, rd);
         // the all-gather: value v = the dot of real column v of block bd (slot S-rd+v),
         // then value rd + l = the Gram term <slot S-rd+l, slot S-1>
@@ -352,17 +359,23 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
             xdone = 0;
         }
         __syncthreads();
+        // value v on wave v (and v + NW, ... when a block has more values than waves):
+        // publish first, then (PFX) the next pass's dot block -- its loads queue behind
+        // the publish, not in front of it -- then collect
+        const int vend = KM <= NW ? (wv < K ? wv + 1 : 0) : K;
+        for (int v = wv; v < vend; v += NW) {
+            double s = sm[v][0];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) s += sm[v][w];
+            res_publish_v(a, xi, v, s);
+        }
         if (p + 2 < P) {  // the next pass reduces dots: its block's loads overlap this all-gather
             const int b2 = (p + 2) % nb1;
             prefetch(blk_lo(b2, S), blk_n(b2, S, j));
         }
-        // value v on wave v (and v + NW, ... when a block has more values than waves)
-        for (int v = wv; v < (KM <= NW ? (wv < K ? wv + 1 : 0) : K); v += NW) {
-            double s = sm[v][0];
-#pragma unroll
-            for (int w = 1; w < NW; ++w) s += sm[v][w];
+        for (int v = wv; v < vend; v += NW) {
             double out = 0.0;
-            const bool okv = res_exchange_v<BLK_POLL_SLEEP>(a, xi, v, s, &out);
+            const bool okv = res_collect_v<BLK_POLL_SLEEP>(a, xi, v, &out);
             if (lane == 0) {
                 bc[v] = out;
                 if (!okv) okf = 0;
@@ -385,7 +398,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
                 }
             }
         }
-        if constexpr (PFX > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA (prefetch, Gram rows) landed
         __syncthreads();
         if constexpr (TCH > 0) asm volatile("s_waitcnt vmcnt(0)" : : "v"(touch_sink) : "memory");
         ++xi;
@@ -395,18 +408,30 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
         // h of block bd (MGS in exact arithmetic), the H column, the new Gram terms
         if (t == 0) {
             double hn[S];
-            for (int k = 0; k < rd; ++k) {
-                double hk = bc[k];
-                for (int l = 0; l < k; ++l) {
-                    const double g = (gram && k == rd - 1) ? bc[rd + l] : gsh[k * S + l];
-                    hk = hk - hn[l] * g;
+#pragma unroll
+            for (int k = 0; k < S; ++k)
+                if (k < rd) {
+                    double hk = bc[k];
+#pragma unroll
+                    for (int l = 0; l < k; ++l) {
+                        const double g = (gram && k == rd - 1) ? bc[rd + l] : gbuf[(k - 1) * RES_SMAX + (k - l)];
+                        hk = hk - hn[l] * g;
+                    }
+                    hn[k] = hk;
                 }
-                hn[k] = hk;
+#pragma unroll
+            for (int s = 0; s < S; ++s) {  // slot s holds real column k = s - (S - rd)
+                double v = 0.0;
+#pragma unroll
+                for (int k = 0; k < S; ++k)
+                    if (k < rd && s == S - rd + k) v = hn[k];
+                hv[s] = v;
             }
-            for (int s = 0; s < S; ++s) hv[s] = s >= S - rd ? hn[s - (S - rd)] : 0.0;
             if (blockIdx.x == 0) {
                 const bool sw1 = p + 1 < nb1;  // block bd is subtracted in the first sweep
-                for (int k = 0; k < rd; ++k) hsh[id + k] = (sw1 ? 0.0 : hsh[id + k]) + hn[k];
+#pragma unroll
+                for (int k = 0; k < S; ++k)
+                    if (k < rd) hsh[id + k] = (sw1 ? 0.0 : hsh[id + k]) + hn[k];
                 if (gram && sw1)
                     for (int l = 0; l < rd - 1; ++l) a.gm[(i64)(j - 1) * RES_SMAX + (rd - 1 - l)] = bc[rd + l];
             }
@@ -465,7 +490,7 @@ struct BlkCfg<2> {
 };
 template <>
 struct BlkCfg<4> {
-    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4}, {8, 0, 8, 0, 512, 2}, {16, 0, 2, 4, 512, 0},
+    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4}, {8, 0, 8, 0, 512, 0}, {16, 0, 2, 4, 512, 0},
                                             {32, 0, 0, 4, 512, 0}, {88, 38, 0, 0, 256, 0}};
     static constexpr int wb[BLK_NVAR] = {4, 2, 2, 1, 2};
 };

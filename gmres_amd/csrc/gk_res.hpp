@@ -454,26 +454,32 @@ constexpr int RES_KMAX = 2 * RES_SMAX - 1;     // its dots + the Gram terms of i
 constexpr i64 RES_GATH_ALL = (i64)RES_KMAX * RES_GATH_WORDS;
 static_assert(RES_KMAX <= XS_REP_STEP, "the values of one exchange must fit a replica's value slots");
 
-// One wave: value v of exchange p, s = this workgroup's partial of it.  Returns
-// false when a deadline passed (*a.err set); *out = the grid (and rank) total,
-// the same bits in every workgroup and on every rank.
+// One wave: publish value v of exchange p (s = this workgroup's partial of it) --
+// its granule pair into every replica, no wait.
+__device__ __forceinline__ void res_publish_v(const ResArgs &a, int p, int v, double s) {
+    const int lane = threadIdx.x & 63;
+    const unsigned tag = a.tag0 + (unsigned)p;
+    if (lane < 2 * RES_NREP) {
+        u64 *gv = a.gath + (i64)v * RES_GATH_WORDS;
+        u64 *q = gv + (RES_NREP > 1 ? RES_REP0 + (lane >> 1) * RES_REP_STRIDE : 0) + (i64)(p & 1) * gridDim.x * 2;
+        const u64 bits = (u64)__double_as_longlong(s);
+        const int half = lane & 1;
+        __hip_atomic_store(q + 2 * blockIdx.x + half, ((u64)tag << 32) | (half ? (unsigned)(bits >> 32) : (unsigned)bits),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// One wave: collect value v of exchange p -- sweep the G partials of this rank's
+// copy (replica blockIdx % NREP; on N ranks workgroup 0 only, then the rank-total
+// hop).  Returns false when a deadline passed (*a.err set); *out = the grid (and
+// rank) total, the same bits in every workgroup and on every rank.
 template <int SLEEP>
-__device__ __forceinline__ bool res_exchange_v(const ResArgs &a, int p, int v, double s, double *out) {
+__device__ __forceinline__ bool res_collect_v(const ResArgs &a, int p, int v, double *out) {
     const int lane = threadIdx.x & 63;
     const int G = gridDim.x;
     const unsigned tag = a.tag0 + (unsigned)p;
-    u64 *gv = a.gath + (i64)v * RES_GATH_WORDS;
-    auto rep_slot = [&](int r) -> u64 * {
-        return gv + (RES_NREP > 1 ? RES_REP0 + r * RES_REP_STRIDE : 0) + (i64)(p & 1) * G * 2;
-    };
-    u64 *slot = rep_slot((int)(blockIdx.x % RES_NREP));
-    if (lane < 2 * RES_NREP) {
-        const u64 bits = (u64)__double_as_longlong(s);
-        const int half = lane & 1;
-        __hip_atomic_store(rep_slot(lane >> 1) + 2 * blockIdx.x + half,
-                           ((u64)tag << 32) | (half ? (unsigned)(bits >> 32) : (unsigned)bits), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const u64 *slot = a.gath + (i64)v * RES_GATH_WORDS +
+                      (RES_NREP > 1 ? RES_REP0 + (int)(blockIdx.x % RES_NREP) * RES_REP_STRIDE : 0) + (i64)(p & 1) * G * 2;
     const u64 deadline = wall_clock64() + a.timeout;
     double acc = 0.0;
     bool all_ok = true;

@@ -93,7 +93,7 @@ def test_blocked_plan_of_every_split(N, R, S, want):
     assert p["variant"] == "blocked" and p["blk"] == S and p["G"] == 256, p
     assert (p["wt"], p["r2e"], p["l2e"], p["r2"], p["l2"]) == want, p
     lw = 38 if p["wt"] == 256 else 0
-    pfx = {(512, 4): 4, (512, 8): 8 if S == 2 else 2}.get((p["wt"], p["r2e"]), 0)  # LDS prefetch of small slabs
+    pfx = {(512, 4): 4, (512, 8): 8 if S == 2 else 0}.get((p["wt"], p["r2e"]), 0)  # LDS prefetch of small slabs
     assert p["lds"] == (lw + S * (p["l2"] + pfx)) * p["wt"] * 16 and p["lds"] + 5 * 1024 <= 160 * 1024, p
     # the whole slab is resident except the w-only S = 4 build's two streamed chunks
     assert p["nres2"] <= N * nl // 2
