@@ -438,9 +438,12 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: d
             fused = sum(res_launch_bytes(plan, nloc, 2 * j, mgs=True, sten=sten) for j in steps_js)
             written = sum(mgs_step_bytes(nloc, j, "as_written", sten) for j in steps_js)
             nproj = sum(2 * j for j in steps_js)
-            kname = ("gk::k_mgs_wres / k_mgs_res (resident MGS-R step: 2j fused projections + norm + scale, one "
-                     "persistent launch per Arnoldi step" + ("; w = A V(:,j) and the first dot formed in the "
-                                                             "launch's prologue)" if sten else ")"))
+            kname = ("gk::k_mgs_wres / k_mgs_wpc / k_mgs_res (resident MGS-R step: 2j fused projections + norm + "
+                     "scale, one persistent launch per Arnoldi step)")
+            if variant == "blocked":
+                kname = (f"gk::k_mgs_blk (blocked-projection MGS-R step, GK_TUNE_RES_BLOCK {plan.get('blk')}: the 2j "
+                         f"projections in blocks of {plan.get('blk')}, one in-launch all-gather per block; one "
+                         "persistent launch per Arnoldi step)")
             timing = f"HIP events on the context stream around the step launch of steps j % {S} == 0 of the timed cycles"
         per_proj = ms * 1e3 / nproj
         model = ("compulsory bytes of the selected resident variant (bench.res_launch_bytes, DESIGN.md §3): per "
@@ -621,8 +624,11 @@ GOLDEN_FALLBACK = {
     "mgsr_omp_cbpr2_4096_m95_2cyc_t8": "mgsr_omp_cbpr2_4096_m95_1cyc_t8",
     "hh_omp_identity_4096_m95_2cyc_t8": "hh_omp_identity_4096_m95_1cyc_t8",
 }
-# (BASELINE configs[] index, grid, precond, degree, method, timed cycles)
-CONFIG_LEGS = [(1, 1024, "identity", 1, "mgsr", 3), (2, 4096, "cheb", 8, "mgsr", 2), (4, 4096, "identity", 1, "hh", 2)]
+# (BASELINE configs[] index, grid, precond, degree, method, timed cycles, MGS projection block)
+# -- block > 1: the same config on the opt-in blocked-projection step (GK_TUNE_RES_BLOCK;
+# the reference's strict MGS-R stays the default everywhere else)
+CONFIG_LEGS = [(1, 1024, "identity", 1, "mgsr", 3, 1), (1, 1024, "identity", 1, "mgsr", 3, 4),
+               (2, 4096, "cheb", 8, "mgsr", 2, 1), (4, 4096, "identity", 1, "hh", 2, 1)]
 
 
 def history_vs_golden(hist, gfile: str | None, gkey: str | None, tol: float = 1e-9, floor: float = 1e-6) -> dict:
@@ -651,10 +657,12 @@ def config_legs(ga, prof_every: int) -> list[dict]:
     x0 = 0 (warmup; its cycle-1 true residual checked against the golden run),
     then K timed cycles of a new solve with HIP events on the dominant kernels."""
     out = []
-    for idx, N, prec, degree, method, K in CONFIG_LEGS:
+    for idx, N, prec, degree, method, K, block in CONFIG_LEGS:
         m = 95
         ns = argparse.Namespace(m=m, method=method, prof_every=prof_every, grid=N, prec=prec, degree=degree)
         with ga.Context(N, m) as c:
+            if block > 1:
+                c.tune(23, block)  # GK_TUNE_RES_BLOCK
             c.set_precond(prec, (8.2, 0.2), degree)
             c.set_rhs_ones()
 
@@ -678,7 +686,10 @@ def config_legs(ga, prof_every: int) -> list[dict]:
             roof = roofline_entry(prof, ns, c.nloc, r.n_cycles, 1, plan, sten) or {}
         iters = (r.n_cycles - 1) * m + r.n_out
         pname = {"identity": "no precond", "cbpr2": "cbpr2", "cheb": f"Chebyshev({degree})"}[prec]
-        leg = {"baseline_config": idx, "workload": f"{N}x{N} Poisson-2D fp64, GMRES-{method.upper()} m={m}, {pname}",
+        blk = f", blocked projections S={block} (opt-in GK_TUNE_RES_BLOCK)" if block > 1 else ""
+        leg = {"baseline_config": idx,
+               "workload": f"{N}x{N} Poisson-2D fp64, GMRES-{method.upper()} m={m}, {pname}{blk}",
+               "projection_block": block,
                "it_s": round(iters / (t1 - t0), 3), "ms_per_cycle": round((t1 - t0) / r.n_cycles * 1e3, 3),
                "cycles": r.n_cycles,
                "dominant": {k: roof.get(k) for k in ("kernel", "variant", "avg_launch_us", "per_projection_us",

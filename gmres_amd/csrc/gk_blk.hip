@@ -30,6 +30,17 @@ __device__ __forceinline__ double uniform(double v) {
 #define GK_BLK_POLL_SLEEP 16
 #endif
 constexpr int BLK_POLL_SLEEP = GK_BLK_POLL_SLEEP;
+#ifndef GK_BLK_REV2
+#define GK_BLK_REV2 1
+#endif
+constexpr bool BLK_REV2 = GK_BLK_REV2 != 0;  // the second sweep's blocks in reverse order (A/B knob)
+#ifndef GK_BLK_DOT_NT
+#define GK_BLK_DOT_NT 0
+#endif
+// 1: the dot columns of cached chunks non-temporal (they are held on chip from then
+// on); 0: the default policy, so a column read again within the Infinity Cache's
+// reach (the reversed second sweep, the next step's first sweep) is a hit (A/B knob)
+constexpr bool BLK_DOT_NT = GK_BLK_DOT_NT != 0;
 #ifndef GK_BLK_WB_LDS
 #define GK_BLK_WB_LDS 2
 #endif
@@ -91,6 +102,11 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
     const int j = a.j;
     const int nb1 = blk_sweep(j, S), P = 2 * nb1;
+    // the block pass p subtracts: the first sweep in column order, the second (REV2)
+    // in reverse -- its first block is the one the first sweep ended with (still on
+    // chip), and the columns read last come back first (Infinity-Cache hits at the
+    // split loads); in exact arithmetic the second sweep's h are all 0 in any order
+    auto blk_of = [&](int p) { return p < nb1 ? p : (BLK_REV2 ? 2 * nb1 - 1 - p : p - nb1); };
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
     const i64 nch = a.nres2 / NT;
     const i64 c0 = (i64)blockIdx.x * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
@@ -152,7 +168,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     }
     for (int k = 0; k < LW; ++k)
         if (l0 + k < lend) lw[k * NT + t] = W2[(l0 + k) * NT + t];
-    prefetch(blk_lo(1 % nb1, S), blk_n(1 % nb1, S, j));  // pass 0's dot block
+    prefetch(blk_lo(blk_of(1), S), blk_n(blk_of(1), S, j));  // pass 0's dot block
     // h of block 0 = <w, V(:,1)>: the operator launch's partial slab (on N ranks
     // its rank hop here, res_pin_fold)
     double h;
@@ -224,7 +240,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
                     for (int d = 0; d < S; ++d) {
                         if (k < PFX)  // (the norm pass reads a stale but finite block here: unused)
                             bv[u][d] = lpf[(d * PFX + (k < PFX ? k : 0)) * NT + t];
-                        else if (k < RX + LX)
+                        else if (k < RX + LX && BLK_DOT_NT)
                             bv[u][d] = ldv<true>(at(D[d], cb + k));
                         else
                             bv[u][d] = ldv<false>(at(D[d], cb + k));
@@ -324,9 +340,9 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     int xi = 0;
     int touch_sink = 0;
     for (int p = 0; p < P && ok; ++p) {
-        const int ba = p % nb1, ia = blk_lo(ba, S), ra = blk_n(ba, S, j);
+        const int ba = blk_of(p), ia = blk_lo(ba, S), ra = blk_n(ba, S, j);
         const bool last = p == P - 1;
-        const int bd = (p + 1) % nb1, id = blk_lo(bd, S), rd = last ? 1 : blk_n(bd, S, j);
+        const int bd = blk_of(p + 1), id = blk_lo(bd, S), rd = last ? 1 : blk_n(bd, S, j);
         const bool gram = !last && bd == nb1 - 1 && rd >= 2;  // the block of the newest column j-1
         // the stored Gram terms of block bd (the newest column's come with this
         // all-gather): rows id+1 .. id+S-1 of the table, straight into LDS by wave 0
@@ -370,7 +386,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
             res_publish_v(a, xi, v, s);
         }
         if (p + 2 < P) {  // the next pass reduces dots: its block's loads overlap this all-gather
-            const int b2 = (p + 2) % nb1;
+            const int b2 = blk_of(p + 2);
             prefetch(blk_lo(b2, S), blk_n(b2, S, j));
         }
         for (int v = wv; v < vend; v += NW) {
@@ -387,7 +403,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
             // 128-B line, paced, until every all-gather wave holds its total
             const int kw = K < NW ? K : NW;
             if (wv >= kw && p + 2 < P) {
-                const int b2 = (p + 2) % nb1;
+                const int b2 = blk_of(p + 2);
                 const int tcol = blk_lo(b2, S) + blk_n(b2, S, j) - 1;
                 const char *base = reinterpret_cast<const char *>(V2 + (i64)tcol * ld2 + c0 * NT);
                 const i64 nc = cend - c0 < TCH ? (cend - c0 > 0 ? cend - c0 : 0) : TCH;

@@ -49,6 +49,26 @@ POINTS = [
     ("4096^2 on 8 GPUs", 8, 4096, 1448, "r04/bench_point_1448_r04k.json"),
     ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r04/bench_point_2896_r04y.json"),
 ]
+# the same points with the opt-in blocked-projection step (GK_TUNE_RES_BLOCK S, round 5):
+# per point the block size that measured fastest at that load, one in-launch all-gather
+# (and so one cross-rank hop) per block of S projections
+POINTS_BLOCKED = [
+    ("4096^2 on 1 GPU", 1, 4096, 4096, "r05/bench_point_4096_blk4_r05b.json", 4),
+    ("4096^2 on 2 GPUs", 2, 4096, 2896, "r05/bench_point_2896_blk2_r05h.json", 2),
+    ("4096^2 on 4 GPUs", 4, 4096, 2048, "r05/bench_point_2048_blk2_r05h.json", 2),
+    ("4096^2 on 8 GPUs", 8, 4096, 1448, "r05/bench_point_1448_blk4_r05h.json", 4),
+    ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r05/bench_point_2896_blk2_r05h.json", 2),
+]
+
+
+def hops_per_cycle(S: int) -> int:
+    """In-launch cross-rank hops of one cycle: per step the first dot's plus one per
+    all-gather -- 2j (strict) or 2 (1 + ceil((j-1)/S)) (blocked, gk_blk.hpp)."""
+    if S <= 1:
+        return M * (M + 2)
+    return sum(1 + 2 * (1 + (j - 1 + S - 1) // S) for j in range(1, M + 1))
+
+
 # {"2": {"allreduce": us, "halo": us}, "4": {...}}: gk_comm_latency of same-device rehearsals
 COMM = "r04/rehearsal_comm_latency_r04d.json"
 
@@ -64,10 +84,12 @@ def load(rel: str) -> dict | None:
         return json.loads([x for x in txt.splitlines() if x.startswith("{")][-1])
 
 
-def predict(hop_lo: float, hop_hi: float, coll_lo: float = 5.0) -> dict:
+def predict(hop_lo: float, hop_hi: float, coll_lo: float = 5.0, blocked: bool = False) -> dict:
     comm = load(COMM) or {}
     rows = []
-    for label, world, grid, g1, rel in POINTS:
+    for pt in (POINTS_BLOCKED if blocked else POINTS):
+        label, world, grid, g1, rel = pt[:5]
+        S = pt[5] if blocked else 1
         cw = comm.get(str(world)) or comm.get(str(max([int(k) for k in comm if k.isdigit()] or [0]))) or {}
         t_ar, t_halo = float(cw.get("allreduce", 10.0)), float(cw.get("halo", 10.0))
         fixed_lo = 0.0 if world == 1 else M * coll_lo * 1e-6
@@ -78,11 +100,12 @@ def predict(hop_lo: float, hop_hi: float, coll_lo: float = 5.0) -> dict:
         t1 = float(b["ms_per_step"]) * 1e-3  # one cycle of the equal-load single-GPU run
         split = ((b.get("diagnostics") or {}).get("resident_split_per_unit_us") or {}).get("mgs_step") or {}
         extra_fixed = 0.0 if world == 1 else M * t_halo * 1e-6
-        nproj = M * (M + 2)  # the 2j projections of every step plus its first dot
+        nproj = hops_per_cycle(S)  # strict: the 2j projections of every step plus its first dot
         lo = t1 + fixed_lo + (0.0 if world == 1 else nproj * hop_lo * 1e-6)
         hi = t1 + extra_fixed + (0.0 if world == 1 else nproj * hop_hi * 1e-6)
         rows.append({
             "point": label, "world": world, "grid": grid, "per_gpu_unknowns": grid * grid // world,
+            "projection_block": S, "hops_per_cycle": nproj if world > 1 else 0,
             "equal_load_grid": g1, "variant": (b.get("config") or {}).get("resident_variant"),
             "t_cycle_1gpu_ms": round(t1 * 1e3, 2),
             "per_projection_1gpu_us": (b.get("roofline") or {}).get("per_projection_us"),
@@ -101,7 +124,8 @@ def predict(hop_lo: float, hop_hi: float, coll_lo: float = 5.0) -> dict:
     for r in rows:
         if base and "predicted_it_s" in r and r["grid"] == 4096:
             r["predicted_speedup"] = [round(v / base["predicted_it_s"][1], 2) for v in r["predicted_it_s"]]
-    return {"model": "t_cycle(N) = t_cycle_1GPU(n/N) + m t_halo + m (m+2) delta_hop (first dot folded into the launch)",
+    return {"model": ("t_cycle(N) = t_cycle_1GPU(n/N) + m t_halo + hops delta_hop (first dot folded into the launch; "
+                      "hops = m (m+2) strict, sum_j 1 + 2 (1 + ceil((j-1)/S)) blocked)"),
             "m": M, "collective_per_call_low_us": coll_lo, "collective_source": f"profiles/{COMM}" if comm else "default 10 us (no rehearsal file)",
             "delta_hop_us": [hop_lo, hop_hi], "points": rows}
 
@@ -111,18 +135,26 @@ def main() -> None:
     ap.add_argument("--hop-lo", type=float, default=1.0)
     ap.add_argument("--hop-hi", type=float, default=4.0)
     ap.add_argument("--coll-lo", type=float, default=5.0)
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04", "scaling_prediction_r04.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05", "scaling_prediction_r05.json"))
     a = ap.parse_args()
-    out = predict(a.hop_lo, a.hop_hi, a.coll_lo)
+    out = {"strict": predict(a.hop_lo, a.hop_hi, a.coll_lo),
+           "blocked": predict(a.hop_lo, a.hop_hi, a.coll_lo, blocked=True)}
     json.dump(out, open(a.out, "w"), indent=1)
-    print("| point | variant | 1-GPU cycle at the per-GPU load (ms) | predicted ms / cycle | predicted it/s |"
+    for name, tab in out.items():
+        print(f"\n{name}:")
+        table(tab)
+
+
+def table(out: dict) -> None:
+    print("| point | variant (S) | 1-GPU cycle at the per-GPU load (ms) | predicted ms / cycle | predicted it/s |"
           " predicted wait / projection (us) |")
     print("|---|---|---|---|---|---|")
     for r in out["points"]:
         if "missing" in r:
             print(f"| {r['point']} | missing {r['missing']} | | | | |")
             continue
-        print(f"| {r['point']} | {r['variant']} | {r['t_cycle_1gpu_ms']} | {r['predicted_ms_per_cycle'][0]}-"
+        print(f"| {r['point']} | {r['variant']} ({r['projection_block']}) | {r['t_cycle_1gpu_ms']} | "
+              f"{r['predicted_ms_per_cycle'][0]}-"
               f"{r['predicted_ms_per_cycle'][1]} | {r['predicted_it_s'][0]}-{r['predicted_it_s'][1]} | "
               f"{r['predicted_wait_per_projection_us']} |")
 
