@@ -57,13 +57,12 @@ METRIC = "Arnoldi iters/sec + HBM GB/s, 4096² Poisson-2D fp64, GMRES(m=95)"
 #    columns it touches, 16n; per resident step launch (32j + 16) n (2j
 #    projections + reading w once + writing V(:,j+1)).  roofline.frac uses it.
 
-def mgs_step_bytes(n: int, j: int, model: str, sten: bool = False) -> float:
-    """One resident MGS-R step launch (cascade + norm + scale).  sten: the launch
-    forms w = A V(:,j) itself and takes the first dot (reads V(:,j) and V(:,1)
-    instead of w: +8n fused); otherwise the stencil is its own launch."""
+def mgs_step_bytes(n: int, j: int, model: str) -> float:
+    """One resident MGS-R step launch (cascade + norm + scale); the stencil is
+    its own launch."""
     if model == "as_written":
-        return float((80 * j + 24 + (16 if sten else 0)) * n)
-    return float((32 * j + 16 + (8 if sten else 0)) * n)
+        return float((80 * j + 24) * n)
+    return float((32 * j + 16) * n)
 
 
 def res_regions(plan: dict, nloc: int) -> dict:
@@ -90,7 +89,7 @@ def res_regions(plan: dict, nloc: int) -> dict:
     return {"pairs": 2 * nreg2, "w_on_chip": 2 * (nres2 - nreg2), "streamed": 2 * (n2 - nres2) + (nloc & 1)}
 
 
-def res_launch_bytes(plan: dict, nloc: int, P: int, mgs: bool = True, sten: bool = False) -> float:
+def res_launch_bytes(plan: dict, nloc: int, P: int, mgs: bool = True) -> float:
     """Compulsory bytes of ONE resident launch of the selected variant running P
     passes (an MGS-R step: P = 2j, the last one closing with ||w||; a Householder
     chain: P = L reflections), per unknown of each region (res_regions):
@@ -100,13 +99,9 @@ def res_launch_bytes(plan: dict, nloc: int, P: int, mgs: bool = True, sten: bool
       w on chip   w in 8, both columns of every pass but the last (no dot
                   partner) 16P - 8, out 8 -> 16P + 8
       streamed    w read + written, both columns, every pass: 32P - 8; the MGS
-                  step then reads w once more and writes V(:,j+1): +16
-    sten: the launch forms w = A V(:,j) itself (reads V(:,j) and V(:,1) instead
-    of w: +8 per resident unknown)."""
+                  step then reads w once more and writes V(:,j+1): +16"""
     r = res_regions(plan, nloc)
     b = r["pairs"] * (8 * P + 16) + r["w_on_chip"] * (16 * P + 8) + r["streamed"] * (32 * P - 8 + (16 if mgs else 0))
-    if sten:
-        b += 8 * (r["pairs"] + r["w_on_chip"])
     return float(b)
 
 
@@ -135,10 +130,8 @@ def prec_bytes(n: int, prec: str, degree: int, model: str, cheb_sten: bool = Tru
     return float(((0 if (passes == 1 and cheb_sten) else 16) + 48 * (passes - 1)) * n)
 
 
-def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str, sten: bool = False,
-                cheb_sten: bool = True) -> float:
-    """One full restart cycle of m Arnoldi steps (sten: the step launches form
-    w = A V(:,j) themselves -- the stencil's 24n become the launch's +8n)."""
+def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str, cheb_sten: bool = True) -> float:
+    """One full restart cycle of m Arnoldi steps."""
     if model == "as_written":  # SURVEY 8(d): per step (40 + 80 j) n, cycle start 64n, update 8(m+2)n
         if method == "hh":
             b = sum((64 + 80 * j) * n for j in range(1, m + 1)) + 64 * n + 8 * (m + 2) * n + 40 * m * n
@@ -150,7 +143,7 @@ def cycle_bytes(n: int, m: int, prec: str, degree: int, method: str, model: str,
         b = sum(hh_chain_bytes(n, j, model) * 2 + st + 40 * n for j in range(1, m + 1))
         b += hh_chain_bytes(n, m, model) + 24 * n + 40 * n
     else:
-        b = sum(mgs_step_bytes(n, j, model, sten) + (0 if sten else st) for j in range(1, m + 1))
+        b = sum(mgs_step_bytes(n, j, model) + st for j in range(1, m + 1))
         b += 40 * n + 8 * (m + 2) * n  # cycle start (b - A x, norm, V_1) + x update
     # the cycle start's application runs after a stencil launch (never stage-0 fused)
     return float(b + m * prec_bytes(n, prec, degree, model, cheb_sten) + prec_bytes(n, prec, degree, model, False))
@@ -390,12 +383,11 @@ def setup_xgmi(ctx, ctl, rank: int, required: bool):
     return None
 
 
-def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: dict | None = None,
-                   sten: bool = False) -> dict | None:
+def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: dict | None = None) -> dict | None:
     """Dominant kernel: its compulsory bytes per launch over its average launch
     time from HIP events on the context stream.  `plan` = gk_res_info of the
     timed context (the resident variant the launches ran: its bytes are
-    res_launch_bytes); sten: the MGS step launch forms w = A V(:,j) itself."""
+    res_launch_bytes)."""
     m = args.m
     on_res = bool(prof) and prof.get("res", (0.0, 0))[1] > 0 and plan is not None and plan.get("variant")
     if not on_res:
@@ -435,8 +427,8 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: d
         else:
             S = max(1, args.prof_every)
             steps_js = [j for j in range(1, m + 1) if j % S == 0] * cycles
-            fused = sum(res_launch_bytes(plan, nloc, 2 * j, mgs=True, sten=sten) for j in steps_js)
-            written = sum(mgs_step_bytes(nloc, j, "as_written", sten) for j in steps_js)
+            fused = sum(res_launch_bytes(plan, nloc, 2 * j, mgs=True) for j in steps_js)
+            written = sum(mgs_step_bytes(nloc, j, "as_written") for j in steps_js)
             nproj = sum(2 * j for j in steps_js)
             kname = ("gk::k_mgs_wres / k_mgs_wpc / k_mgs_res (resident MGS-R step: 2j fused projections + norm + "
                      "scale, one persistent launch per Arnoldi step)")
@@ -480,13 +472,13 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: d
         if args.method == "hh":
             dram = sum((8.0 * L + 16.0) * nloc for L in chains)
         else:
-            dram = sum((16.0 * j + 16.0 + (8.0 if sten else 0.0)) * nloc for j in steps_js)
+            dram = sum((16.0 * j + 16.0) * nloc for j in steps_js)
         roof["ceiling"] = ("fabric: L2 <-> Infinity Fabric read rate (Infinity-Cache hits included); the DRAM "
                            "side carries about half of these bytes")
         roof["hbm"] = {"bytes_per_launch_est": round(dram / launches), "achieved": round(dram / secs / 1e9, 1),
                        "peak": HBM_PEAK_GBPS, "frac": round(dram / secs / 1e9 / HBM_PEAK_GBPS, 4),
-                       "model": "each pass's dot column from HBM, its AXPY column from the Infinity Cache; w (or, "
-                                "forming w in the launch, V(:,j) and V(:,1)) in, the output column out",
+                       "model": "each pass's dot column from HBM, its AXPY column from the Infinity Cache; w in, "
+                                "the output column out",
                        "evidence": "profiles/r03/ab_qnt_r03d.jsonl (V_q non-temporal: +9.7 % per projection)"}
     else:
         roof["ceiling"] = "hbm: every compulsory byte is a DRAM byte (non-temporal column loads / register reuse)"
@@ -495,8 +487,6 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: d
         key, scale = pmc_lookup(json.load(open(tf)), variant, nloc, m, args.prec, args.method,
                                 int((plan or {}).get("G", 256)))
         pm = json.load(open(tf)).get(key) if key else None
-        if pm and bool(pm.get("sten", False)) != sten:  # measured on the other step flow: not this kernel's bytes
-            pm = None
         if pm and "per_step" in pm:
             per_step = {int(k): v * scale for k, v in pm["per_step"].items()}
             if all(j in per_step for j in set(steps_js)):
@@ -682,8 +672,7 @@ def config_legs(ga, prof_every: int) -> list[dict]:
             t1 = time.perf_counter()
             prof = c.profile_read()
             plan = c.res_info(hh=method == "hh")
-            sten = method == "mgsr" and plan.get("sten", 0) == 1
-            roof = roofline_entry(prof, ns, c.nloc, r.n_cycles, 1, plan, sten) or {}
+            roof = roofline_entry(prof, ns, c.nloc, r.n_cycles, 1, plan) or {}
         iters = (r.n_cycles - 1) * m + r.n_out
         pname = {"identity": "no precond", "cbpr2": "cbpr2", "cheb": f"Chebyshev({degree})"}[prec]
         blk = f", blocked projections S={block} (opt-in GK_TUNE_RES_BLOCK)" if block > 1 else ""
@@ -892,9 +881,8 @@ def main() -> None:
     if diag is not None:
         diag["pcie_inclusive"] = pcie_inclusive(ctx, args, run, ctl, line0, nlines)
 
-    sten = args.method == "mgsr" and plan.get("sten", 0) == 1
     cheb_sten = plan.get("cheb_sten", 0) == 1
-    roof = roofline_entry(prof, args, ctx.nloc, cycles, world, plan, sten) if rank == 0 else None
+    roof = roofline_entry(prof, args, ctx.nloc, cycles, world, plan) if rank == 0 else None
     runtime = ga.runtime_info()
     ctx.close()
     legs = None
@@ -906,8 +894,8 @@ def main() -> None:
         n = N * N
         it_s = iters / elapsed
         full = cycles == args.steps and res.n_out == m
-        b_fused = cycle_bytes(n, m, args.prec, args.degree, args.method, "fused", sten, cheb_sten) * cycles
-        b_written = cycle_bytes(n, m, args.prec, args.degree, args.method, "as_written", sten) * cycles
+        b_fused = cycle_bytes(n, m, args.prec, args.degree, args.method, "fused", cheb_sten) * cycles
+        b_written = cycle_bytes(n, m, args.prec, args.degree, args.method, "as_written") * cycles
         cpu = None
         if not args.no_cpu and world == 1:
             log("CPU baseline (the reference on this host)")

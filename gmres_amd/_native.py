@@ -145,15 +145,31 @@ class _TorchAfterNative:
     libamdhip64 / libhsa-runtime64 / librccl and loads them by path, so
     importing it now would put a second HIP runtime into the process (measured:
     the process aborts at exit, "double free or corruption").  Fail at the
-    import instead, with the remedy."""
+    import instead, with the remedy.  A probe (importlib.util.find_spec) is
+    answered as without the guard -- torch's real spec, or None -- and only
+    loading the module raises: optional-dependency checks elsewhere keep working."""
 
     def find_spec(self, name, path=None, target=None):
-        if name == "torch":
-            raise ImportError("gmres_amd already runs on " + (runtime_paths().get("hip") or "/opt/rocm's HIP runtime")
-                              + "; importing torch now would load torch's bundled HIP runtime as a second one. "
-                                "Import torch before gmres_amd's first native call (then torch's runtime is "
-                                "used), or keep this process torch-free.")
-        return None
+        if name != "torch":
+            return None
+        import importlib.machinery
+        import importlib.util
+
+        real = importlib.machinery.PathFinder.find_spec(name, path)
+        if real is None:
+            return None
+        return importlib.util.spec_from_loader(name, _RefuseTorchLoader(), origin=real.origin)
+
+
+class _RefuseTorchLoader:
+    def create_module(self, spec):
+        raise ImportError("gmres_amd already runs on " + (runtime_paths().get("hip") or "/opt/rocm's HIP runtime")
+                          + "; importing torch now would load torch's bundled HIP runtime as a second one. "
+                            "Import torch before gmres_amd's first native call (then torch's runtime is "
+                            "used), or keep this process torch-free.")
+
+    def exec_module(self, module):  # not reached: create_module raises
+        raise ImportError("torch import refused")
 
 
 def runtime_paths() -> dict:

@@ -1533,7 +1533,12 @@ int mgs_chain(gk_ctx *c, int j, int np) {
 
 // Capture mgs_chain(j) once as a graph (its kernel arguments and communicator
 // calls depend only on j, np and the context's fixed buffers).  A capture that
-// fails switches graphs off for this context; the step then runs call by call.
+// fails switches graphs off for this context; one rank then runs the step call by
+// call.  With an RCCL communicator the failure is an error instead: the discarded
+// graph may already hold some of the step's ncclAllReduce calls, and whether RCCL's
+// per-communicator operation counters stay matched when one rank runs eagerly while
+// its peers replay is not pinned -- the caller reruns with GK_TUNE_GRAPH 0 on every
+// rank.  (GK_DEBUG_CAPTURE_FAIL=1 makes every capture fail after it ends, for tests.)
 int capture_step(gk_ctx *c, int j, int np) {
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
     c->capturing = true;
@@ -1550,11 +1555,21 @@ int capture_step(gk_ctx *c, int j, int np) {
     hipError_t e2 = hipErrorUnknown;
     if (rc == GK_OK && e == hipSuccess && g != nullptr) e2 = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
     if (g != nullptr) (void)hipGraphDestroy(g);
-    if (rc != GK_OK || e != hipSuccess || e2 != hipSuccess) {
-        const std::string why = rc != GK_OK ? g_err : hipGetErrorString(e != hipSuccess ? e : e2);
+    const char *dbg = std::getenv("GK_DEBUG_CAPTURE_FAIL");
+    const bool forced = dbg != nullptr && dbg[0] == '1';
+    if (rc != GK_OK || e != hipSuccess || e2 != hipSuccess || forced) {
+        const std::string why = rc != GK_OK ? g_err
+                                : forced   ? std::string("GK_DEBUG_CAPTURE_FAIL")
+                                           : hipGetErrorString(e != hipSuccess ? e : e2);
         (void)hipGetLastError();
+        if (ge != nullptr) (void)hipGraphExecDestroy(ge);
         c->tune_graph = 0;
         graph_reset(c);
+        if (c->comm != nullptr && !c->xs_on && c->lg == nullptr)  // the step's all-reduces are RCCL calls
+            return set_err(GK_ERR_COMM,
+                           "capture of launch-path step %d failed on an RCCL rank (%s): rerun with GK_TUNE_GRAPH 0 "
+                           "on every rank (one rank running the step eagerly while its peers replay graphs is not "
+                           "supported)", j, why.c_str());
         set_err(GK_OK, "launch-path step graphs off for this context: capture of step %d failed (%s)", j,
                 why.c_str());
         return GK_OK;

@@ -172,7 +172,7 @@ __global__ __launch_bounds__(TPB) void k_scale(double *__restrict__ out, const d
 }
 
 // out[0] = NORM2(x(0:n)) as flang-rt computes it (Norm2Accumulator<8>: a running
-// max m and a scaled sum s, result m sqrt(1 + s); oracle/gmres_oracle.c or_norm2) --
+// max m and a scaled sum s, result m sqrt(1 + s); the tests check it against the CPU restatement) --
 // the reference's serial norm2 of gmres_hh.f90:251-253,307,315, in its order.  One
 // workgroup: chunks of TPB elements staged through LDS, thread 0 folds each in order
 // (GK_TUNE_HH_NORM_ORDER, single rank; ~2 us per 256 elements).

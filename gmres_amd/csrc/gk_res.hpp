@@ -276,7 +276,23 @@ constexpr int RES_POLL_SLEEP = GK_RES_POLL_SLEEP;
 // completes, polls its granules without the sleep (its detection delay is on
 // every rank's critical path; the other workgroups' is not).
 constexpr bool RES_PUSHER_FAST = GK_RES_PUSHER_FAST != 0;
-// N ranks: only workgroup 0 sweeps the local granules (every workgroup reads the R
+#ifndef GK_RES_PUSHERS
+#define GK_RES_PUSHERS 4
+#endif
+// N ranks: workgroups 0 .. RES_PUSHERS-1 (one per XCD under round-robin dispatch)
+// each sweep this rank's granules and push the same rank total (same bits, same
+// sequence tag) into every peer slot, so a total lands as soon as the FIRST of them
+// has seen the sweep complete.  A pusher's stores are complete before it publishes
+// its next partial (s_waitcnt below), so no push of exchange p can land on a slot
+// after the same-parity push of exchange p + 2.  Same-device rehearsals, 1 / 4 / 8
+// pushers, three alternating samples (profiles/r05/ab_pushers_r05j.jsonl; every run
+// the same bits): wait per projection 2 ranks 2896^2 4.67 / 4.57 / 4.58 us (one
+// outlier of 1 and 8 dropped), 4 ranks 2048^2 4.01 / 3.93 / 4.02, 2 ranks 1448^2
+// 3.81 / 3.79 / 3.89 -- a small gain at 4, none at 8.
+constexpr int RES_PUSHERS = GK_RES_PUSHERS;
+static_assert(RES_PUSHERS >= 1 && RES_PUSHERS <= 8, "1..8 rank-total pushers");
+__device__ __forceinline__ bool res_pusher(const ResArgs &a) { return a.nranks > 1 && blockIdx.x < RES_PUSHERS; }
+// N ranks: only the pushers (workgroup 0 by default) sweep the local granules (every workgroup reads the R
 // rank totals, its own rank's among them).  Round 5 removed the A/B knob that let
 // every workgroup sweep (GK_RES_SWEEP_ALL): the same bits, a tie in the same-device
 // rehearsals (profiles/r04/ab_sweep_r04x.jsonl: 605 / 601, 1,094 / 1,093, 1,546 /
@@ -294,13 +310,13 @@ constexpr int RES_POLL_SLEEP_PC = GK_RES_POLL_SLEEP_PC;
 // XS_REP_STEP * r + v of each replica r.
 __device__ __forceinline__ double res_rank_sum(const ResArgs &a, int p, double acc, bool &all_ok, int v = 0) {
     const int lane = threadIdx.x & 63;  // any one wave of the workgroup (value v on wave v in k_mgs_blk)
-    // Rank totals: workgroup 0 pushes this rank's total into every peer's region,
+    // Rank totals: the pushers (workgroup 0 by default) push this rank's total into every peer's region,
     // once per replica (value slot XS_REP_STEP * r of its source row: a line of its
     // own), and every workgroup reads replica blockIdx % NREP -- 1/NREP of the grid
     // polls each line instead of all of it.  A slot is rewritten two exchanges later
     // at the earliest, after every workgroup of every rank has read it (rendezvous).
     const unsigned seq = a.xseq0 + 1u + (unsigned)p, par = seq & 1u;
-    if (blockIdx.x == 0) {
+    if (blockIdx.x < RES_PUSHERS) {
         const u64 bits = (u64)__double_as_longlong(acc);
         for (int k = lane; k < 2 * RES_NREP * a.nranks; k += 64) {
             const int dst = k / (2 * RES_NREP), r = (k >> 1) % RES_NREP, half = k & 1;
@@ -362,6 +378,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
     for (int w = 1; w < NW; ++w) s += sm[w];
     u64 t_pub = 0;
     if (TR && a.trace != nullptr) t_pub = wall_clock64();
+    if (RES_PUSHERS > 1 && res_pusher(a)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last push landed
     if (lane < 2 * RES_NREP) {  // lane 2r + h: half h of the partial into replica r
         const u64 bits = (u64)__double_as_longlong(s);
         const int half = lane & 1;
@@ -372,8 +389,8 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
     const u64 deadline = wall_clock64() + a.timeout;
     double acc = 0.0;
     bool all_ok = true;
-    if (a.nranks == 1 || blockIdx.x == 0) {
-        // (N ranks: only workgroup 0, the pusher, needs this rank's total -- every
+    if (a.nranks == 1 || blockIdx.x < RES_PUSHERS) {
+        // (N ranks: only the pushers need this rank's total -- every
         // workgroup then reads the R rank totals, its own rank's included, so the
         // others skip the sweep and its polls stay off the stragglers' memory path.)
         // Lane L holds granule L + 64k of each 512-granule sweep: the lo (even L)
@@ -413,7 +430,7 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
                     if (lane == 0) xs_fail(a.err, XSE_RES_WG, miss);
                     break;
                 }
-                if (RES_PUSHER_FAST && a.nranks > 1 && blockIdx.x == 0)
+                if (RES_PUSHER_FAST && res_pusher(a))
                     __builtin_amdgcn_s_sleep(1);  // the rank-total pusher: push as soon as the sweep completes
                 else
                     __builtin_amdgcn_s_sleep(SLEEP);
@@ -470,7 +487,7 @@ __device__ __forceinline__ void res_publish_v(const ResArgs &a, int p, int v, do
 }
 
 // One wave: collect value v of exchange p -- sweep the G partials of this rank's
-// copy (replica blockIdx % NREP; on N ranks workgroup 0 only, then the rank-total
+// copy (replica blockIdx % NREP; on N ranks the pushers only, then the rank-total
 // hop).  Returns false when a deadline passed (*a.err set); *out = the grid (and
 // rank) total, the same bits in every workgroup and on every rank.
 template <int SLEEP>
@@ -483,7 +500,8 @@ __device__ __forceinline__ bool res_collect_v(const ResArgs &a, int p, int v, do
     const u64 deadline = wall_clock64() + a.timeout;
     double acc = 0.0;
     bool all_ok = true;
-    if (a.nranks == 1 || blockIdx.x == 0) {
+    if (a.nranks == 1 || blockIdx.x < RES_PUSHERS) {  // (k_mgs_blk: every wave's stores drain before the
+                                                     // barrier that ends an exchange, ahead of the next publish)
         for (int c0 = 0; c0 < 2 * G && all_ok; c0 += 512) {
             unsigned d[8];
             for (;;) {
@@ -514,7 +532,7 @@ __device__ __forceinline__ bool res_collect_v(const ResArgs &a, int p, int v, do
                     break;
                 }
                 if (RES_PUSHER_FAST && a.nranks > 1)
-                    __builtin_amdgcn_s_sleep(1);  // workgroup 0, the rank-total pusher
+                    __builtin_amdgcn_s_sleep(1);  // a rank-total pusher
                 else
                     __builtin_amdgcn_s_sleep(SLEEP);
             }

@@ -186,6 +186,41 @@ def test_launch_path_step_graphs(monkeypatch, rccl):
           f"{t1 / cyc * 1e3:.2f} ms/cycle replayed graphs")
 
 
+@pytest.mark.parametrize("rccl", [False, True])
+def test_launch_path_capture_failure(monkeypatch, rccl):
+    """A step-graph capture that fails (forced: GK_DEBUG_CAPTURE_FAIL) switches graphs
+    off for a single-rank context, which then runs call by call with the same bits;
+    on an RCCL rank it is an error naming the remedy (GK_TUNE_GRAPH 0 on every rank),
+    since one rank running eagerly while its peers replay is not supported."""
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+
+    N, m = 256, 30
+    if rccl:
+        monkeypatch.setenv("GK_FORCE_RCCL", "1")
+
+    def run(fail):
+        if fail:
+            monkeypatch.setenv("GK_DEBUG_CAPTURE_FAIL", "1")
+        else:
+            monkeypatch.delenv("GK_DEBUG_CAPTURE_FAIL", raising=False)
+        with ga.Context(N, m) as c:
+            if rccl:
+                c.comm_init(1, 0, N, ga.Context.unique_id())
+            c.tune(nat.GK_TUNE_RES, 0)
+            c.tune(nat.GK_TUNE_GRAPH, 1)
+            c.set_rhs_ones()
+            return ga.gmres_mgsr(c, 1e-15, max_cycles=2, want_hist=True, want_verr=False)
+
+    ref = run(False)
+    if rccl:
+        with pytest.raises(ga.GkError, match="GK_TUNE_GRAPH 0"):
+            run(True)
+    else:
+        r = run(True)
+        assert np.array_equal(r.hist_res, ref.hist_res) and np.array_equal(r.x, ref.x)
+
+
 @pytest.mark.parametrize("R", [2, 3])
 def test_launch_path_step_graphs_device_exchange(R):
     """GK_TUNE_GRAPH over the device exchange (in-process slab ranks, resident

@@ -125,14 +125,15 @@ def test_torch_import_after_native_load_is_refused(built):
     """The product never imports torch; once libgmres_hip.so runs on /opt/rocm's
     HIP runtime in a torch-free process, importing torch (which would map its
     bundled runtime as a second one and abort at exit) fails at the import."""
-    code = ("import gmres_amd._native as n; n.hip()\n"
+    code = ("import importlib.util, gmres_amd._native as n; n.hip()\n"
+            "print('PROBE', importlib.util.find_spec('torch') is not None)\n"  # probes answered, not refused
             "try:\n    import torch\n    print('IMPORTED')\n"
-            "except ImportError as e:\n    print('REFUSED', 'second one' in str(e))\n")
+            "except ImportError as e:\n    print('REFUSED', 'second one' in str(e), 'torch' in __import__('sys').modules)\n")
     env = dict(os.environ)
     env.pop("GK_TORCH_FIRST", None)
     p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
-    assert p.stdout.split() == ["REFUSED", "True"], p.stdout
+    assert p.stdout.split() == ["PROBE", "True", "REFUSED", "True", "False"], p.stdout
     # torch first, then the library: torch's runtime serves both (one runtime)
     code2 = "import torch, gmres_amd._native as n; n.hip(); print('OK', 'torch' in n.runtime_paths().get('hip', 'torch'))"
     p = subprocess.run([sys.executable, "-c", code2], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)

@@ -59,7 +59,7 @@ def res_fit(a):
     plan = ga.res_plan_query(a.grid * nl, 256, 1, a.method == "hh", -1)
     if a.variant and plan["variant"] != a.variant:
         raise SystemExit(f"the plan query selects {plan['variant']}, not {a.variant}")
-    model = {int(j): bench.res_launch_bytes(plan, n, 2 * int(j), mgs=True, sten=a.sten) for j in js}
+    model = {int(j): bench.res_launch_bytes(plan, n, 2 * int(j), mgs=True) for j in js}
     entry = {"kernel": a.kernel, "variant": plan["variant"], "nloc": n, "G": int(plan["G"]),
              "launches_sampled": int(a.probe_m),
              "bytes_fixed": float(c),
@@ -67,7 +67,6 @@ def res_fit(a):
              "fit_residual_max_rel": float(np.max(np.abs(y - (b * 2 * js + c)) / y)),
              "per_step": {str(int(j)): float(v) for j, v in zip(js, y)},
              "per_step_model_ratio": {str(int(j)): float(v / model[int(j)]) for j, v in zip(js, y) if j % 16 == 0},
-             "sten": bool(a.sten),
              "source": f"{os.path.relpath(a.fetch)} + {os.path.relpath(a.write)} (every launch j = 1..{a.probe_m} "
                        "of one full cycle, FETCH_SIZE x2 gfx950 correction; L2<->fabric bytes incl. "
                        "Infinity-Cache hits)"}
@@ -92,8 +91,6 @@ def main():
                          "fit bytes per launch = fixed + per_projection * 2j")
     ap.add_argument("--probe-m", type=int, default=95, help="resident launches of the traced cycle (= m)")
     ap.add_argument("--variant", default=None, help="the resident variant expected to have run (checked)")
-    ap.add_argument("--sten", action="store_true",
-                    help="the step launches formed w = A V(:,j) themselves (gk_res_info sten; model +8n)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
