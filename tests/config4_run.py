@@ -16,10 +16,13 @@ contexts joined by one of the two multi-rank transports:
          Arnoldi step is ONE launch per rank whose 2j projections sum the 8
          rank totals inside the launch -- the in-launch cross-rank path the
          8-GPU run takes (there with 256 workgroups per rank).
+  xchg-res-blk2  the same with the opt-in blocked-projection step (GK_TUNE_RES_BLOCK 2:
+         one in-launch all-gather, and so one rank-total hop, per block of 2
+         projections; exact-arithmetic MGS, pinned to the same reference cycle).
 
 Prints one JSON line: the single run's and rank 0's residual / final_err,
 whether every rank took identical decisions, and the largest deviations.
-  python tests/config4_run.py local|xchg|xchg-res
+  python tests/config4_run.py local|xchg|xchg-res|xchg-res-blk2
 """
 from __future__ import annotations
 
@@ -54,12 +57,14 @@ def run(transport: str, cycles: int = CYCLES) -> dict:
         ml = max(nl for _, nl in parts)
         for r, c in enumerate(ctxs):
             c.comm_init_local(g, r, ml)
-        if transport in ("xchg", "xchg-res"):
+        if transport.startswith("xchg"):
             for c in ctxs:
                 c.xchg_local()
                 c.tune(nat.GK_TUNE_XCHG_TIMEOUT_MS, 20000)
-        if transport == "xchg-res":
+        if transport.startswith("xchg-res"):
             for c in ctxs:
+                if transport == "xchg-res-blk2":
+                    c.tune(nat.GK_TUNE_RES_BLOCK, 2)
                 c.tune(nat.GK_TUNE_RES, 1)
                 c.tune(nat.GK_TUNE_RES_SHARE, R)
                 c.tune(nat.GK_TUNE_RES_TIMEOUT_MS, 20000)

@@ -112,7 +112,7 @@ def test_4096_two_cycle_history_vs_reference(method, prec, key):
         assert a == pytest.approx(b, rel=1e-9), (r.hist_res[:2], g)
 
 
-@pytest.mark.parametrize("transport", ["local", "xchg", "xchg-res"])
+@pytest.mark.parametrize("transport", ["local", "xchg", "xchg-res", "xchg-res-blk2"])
 def test_config4_8192_eight_row_block_ranks_on_one_gpu(transport):
     """Config 4's decomposition (8 slabs of 1024 grid lines, per-projection
     all-reduce of the partial slabs, halo lines before every stencil) against a
@@ -121,7 +121,9 @@ def test_config4_8192_eight_row_block_ranks_on_one_gpu(transport):
     (tests/config4_run.py; a child process with GPU_MAX_HW_QUEUES=16 so that
     the eight ranks' streams run concurrently) -- on the launch path, and
     (xchg-res) with the resident step forced on, 32 workgroups per rank, so the
-    8 rank totals of every projection are summed inside the step launch.  The
+    8 rank totals of every projection are summed inside the step launch
+    (xchg-res-blk2: the opt-in blocked-projection step, one all-gather and rank
+    hop per 2 projections, against the same reference cycle at 1e-9).  The
     single-context run itself
     is pinned to the reference's own 8192^2 cycle (tests/golden/make_ref_8192.py,
     the reference built from its sources, run on the GPU box's host).  Only the
@@ -140,7 +142,7 @@ def test_config4_8192_eight_row_block_ranks_on_one_gpu(transport):
     assert r["ok"], r
     assert r["comm_kinds"] == (["local-group"] if transport == "local" else ["xgmi-device-exchange"]), r
     assert r["comm_launches"] > 0 and r["same_decisions"] and r["n_out"] == 95, r
-    if transport == "xchg-res":
+    if transport.startswith("xchg-res"):
         # every Arnoldi step one resident launch per rank, no per-projection launch or
         # all-reduce call: the all-reduce launches left are, per cycle, one per step (the
         # stencil's fused first dot), the cycle start's norm and the history's true
@@ -148,6 +150,8 @@ def test_config4_8192_eight_row_block_ranks_on_one_gpu(transport):
         cyc = len(r["hist_res"])
         assert r["res_G"] == [32] and r["res_launches_min"] >= 95 * cyc and r["proj_launches_max"] <= 1, r
         assert r["comm_launches_max"] <= cyc * (95 + 2) + 1, r
+        if transport.endswith("blk2"):
+            assert r["res_variants"] == ["blocked"], r
     else:
         assert r["res_launches_min"] == 0, r
     assert r["hist_res0"] == pytest.approx(r["ref_hist_res0"], rel=1e-9), r
