@@ -701,9 +701,16 @@ constexpr int RES_L2 = 18;              // LDS-resident double2 of w per data th
 constexpr int RES_R2_BIG = 12;          // two register arrays of 12 double2 fit 256 VGPRs without spills
 
 #ifndef GK_RES_RW
-#define GK_RES_RW 88
+#define GK_RES_RW 89
 #endif
-constexpr int RES_RW = GK_RES_RW, RES_LW = 38;  // w-only variant: double2 of w per thread in registers / LDS
+#ifndef GK_RES_LW
+#define GK_RES_LW 39
+#endif
+// w-only variant: double2 of w per thread in registers / LDS.  The MGS step holds 89 + 39
+// chunks -- the whole 4096^2 slab on chip, nothing streamed -- since round 5 sized its H
+// column in LDS by m (gk::WO_HMAX) instead of RHMAX; rounds 1-4 held 88 + 38 and streamed
+// 1.5 % of w at 32 B per unknown.  The reflection chains keep 90 + 38 (RES_RW_HH, RES_LW_HH).
+constexpr int RES_RW = GK_RES_RW, RES_LW = GK_RES_LW, RES_LW_HH = 38;
 #ifndef GK_RES_RW_HH
 #define GK_RES_RW_HH 90
 #endif
@@ -798,7 +805,7 @@ i64 pairs_bytes(i64 n2, int G) {  // k_mgs_res<12, 18>: 2 x 12 registers + 18 LD
 }
 
 i64 wonly_bytes(i64 n2, int G) {
-    const i64 rw = (i64)G * (RES_RW + RES_LW) * gk::WT;
+    const i64 rw = (i64)G * (RES_RW + RES_LW) * gk::WT;  // (the MGS step's; the reflection chains' is the same 128)
     const i64 wr = std::min(n2, rw), ws = n2 > rw ? n2 - rw : 0;
     return 16 * wr + 32 * ws;
 }
@@ -885,8 +892,8 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         p.wo = true;
         p.wt = gk::WT;
         p.r2 = 0;  // (the kernel's register part is RES_RW / RES_RW_HH chunks: r2e)
-        spread(gk::WT, hh ? RES_RW_HH : RES_RW, RES_LW);
-        p.lds = RES_LW * gk::WT * (int)sizeof(double2);
+        spread(gk::WT, hh ? RES_RW_HH : RES_RW, hh ? RES_LW_HH : RES_LW);
+        p.lds = (hh ? RES_LW_HH : RES_LW) * gk::WT * (int)sizeof(double2);
         p.nt = true;  // V_i non-temporal, V_q default policy (fixed in the kernel)
         return;
     } else {
@@ -920,6 +927,7 @@ bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
     const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : RES_R2_BIG;
     plan_resident(c->nloc, gmax, cap, c->tune_res_lds, c->tune_res_wonly, hh,
                   c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p, c->tune_res_pc, c->tune_res_blk);
+    if (p.wo && !hh && c->m + 1 > gk::WO_HMAX) return false;  // its H column: WO_HMAX entries of LDS
     return true;
 }
 
@@ -977,15 +985,16 @@ int launch_res_t(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 template <int MODE>
 int launch_wres_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     constexpr int RW = MODE == gk::RES_MGS ? RES_RW : RES_RW_HH;
+    constexpr int LW = MODE == gk::RES_MGS ? RES_LW : RES_LW_HH;
     constexpr int WBT = MODE == gk::RES_MGS ? gk::WB : gk::WB_HH;
     static std::atomic<int> attr[ATTR_DEVS];
     if (c->dev < 0 || c->dev >= ATTR_DEVS) return set_err(GK_ERR_ARG, "device id %d out of range", c->dev);
     if (attr[c->dev].load() < p.lds) {
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RW, RES_LW, MODE, WBT>),
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&gk::k_mgs_wres<RW, LW, MODE, WBT>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, p.lds));
         attr[c->dev] = p.lds;
     }
-    gk::k_mgs_wres<RW, RES_LW, MODE, WBT><<<p.G, gk::WT, p.lds, c->st>>>(a);
+    gk::k_mgs_wres<RW, LW, MODE, WBT><<<p.G, gk::WT, p.lds, c->st>>>(a);
     LAUNCHCHK();
     return GK_OK;
 }

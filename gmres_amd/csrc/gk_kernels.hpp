@@ -1156,8 +1156,10 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     __shared__ double sm[WT / 64];
     __shared__ double bc[1];
     __shared__ int okf;
-    __shared__ double hsh[RHMAX + 1];
     __shared__ int xdone;  // PACE: the exchange in progress has completed
+    // H(1:j, j): WO_HMAX entries, not RHMAX + 1 -- the MGS step's 39 LDS chunks of w leave
+    // 4,048 bytes of the CU's 160 KiB (res_plan keeps m + 1 <= WO_HMAX on this kernel)
+    __shared__ double hsh[MODE == RES_MGS ? WO_HMAX : 1];
     const int t = threadIdx.x;
     constexpr int mode = MODE;
     constexpr int PACE = MODE == RES_MGS ? TOUCH_PACE : TOUCH_PACE_HH;

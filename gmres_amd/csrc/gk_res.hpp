@@ -102,6 +102,7 @@ constexpr int RT = 512;       // threads per resident workgroup (8 waves, 2 per 
 constexpr int RWAVES = RT / 64;
 constexpr int RGMAX = 1024;   // max workgroups of a resident launch
 constexpr int RHMAX = 512;    // max m on the resident path (H column in LDS)
+constexpr int WO_HMAX = 500;  // ... on the w-only MGS step (its LDS holds 39 chunks of w: k_mgs_wres)
 
 struct ResArgs {
     double *w;            // w = M^-1 A V(:,j) from the operator launch; streamed part in/out

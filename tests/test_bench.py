@@ -82,14 +82,14 @@ def _plan(N, R=1, share=1, nt=-1):
 
 def test_resident_byte_model_follows_the_variant():
     """res_launch_bytes charges each variant what it moves: the w-only kernel 16 B
-    per unknown per pass (+ its streamed 2 %), the pairs kernels 8 B per unknown
-    whose running column sits in registers and 16 B per LDS-held unknown."""
-    n, p = _plan(4096)  # bench default: w-only, 126 of 128 chunks per workgroup on chip
+    per unknown per pass (nothing streamed since round 5), the pairs kernels 8 B per
+    unknown whose running column sits in registers and 16 B per LDS-held unknown."""
+    n, p = _plan(4096)  # bench default: w-only, all 128 chunks per workgroup on chip (89 + 39)
     assert p["variant"] == "w-only"
     r = bench.res_regions(p, n)
-    assert sum(r.values()) == n and r["pairs"] == 0 and r["streamed"] / n < 0.02
+    assert sum(r.values()) == n and r["pairs"] == 0 and r["streamed"] == 0
     per_pass = (bench.res_launch_bytes(p, n, 97) - bench.res_launch_bytes(p, n, 96)) / n
-    assert 16.0 < per_pass < 16.4
+    assert per_pass == 16.0
     # 4096^2 / 2 and 8192^2 / 8 (k_mgs_wpc, 512 threads, the MGS step): w in registers, 25 of
     # its 32 chunks' column cached (8 B per unknown), the other 7 read V_i too (16 B) -> 9.75 B
     n, p = _plan(4096, 2)

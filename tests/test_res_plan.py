@@ -22,7 +22,7 @@ def _plan(N, R, share=1, hh=False, nt=-1):
 
 @pytest.mark.parametrize("hh", [False, True])
 @pytest.mark.parametrize("N,R,variant,r2e,l2e,nt", [
-    (4096, 1, "w-only", None, 38, 1),      # the bench line (config 1), config 3 and 5
+    (4096, 1, "w-only", None, None, 1),    # the bench line (config 1), config 3 and 5
     (4096, 2, "w+column", 32, 0, 1),       # 8.4 M unknowns per GPU: w in registers, its column cached
     (4096, 4, "w+column", 16, 0, 1),       # 4.2 M (8 vs 10 B/unknown of k_mgs_res<12,4>)
     (4096, 8, "pairs", 8, 0, 0),           # 2.1 M (w+column ties at 8 B/unknown: the older kernel kept)
@@ -32,7 +32,7 @@ def _plan(N, R, share=1, hh=False, nt=-1):
 def test_production_splits(N, R, variant, r2e, l2e, nt, hh):
     p = _plan(N, R, hh=hh)
     assert p["variant"] == variant and p["G"] == 256
-    assert p["l2e"] == l2e and p["nt"] == nt
+    assert p["l2e"] == (l2e if l2e is not None else (38 if hh else 39)) and p["nt"] == nt
     if variant == "w+column":  # 512 threads: 4 register + 19 LDS chunks of the column cached;
         # slabs of <= 16 chunks per thread: the 16-chunk kernel, the whole column in registers
         # (the MGS step caches 6 register chunks, the reflection chains 4)
@@ -40,8 +40,10 @@ def test_production_splits(N, R, variant, r2e, l2e, nt, hh):
         assert (p["r2"], p["l2"], p["lds"], p["wt"]) == want + (512,)
     if r2e is not None:
         assert p["r2e"] == r2e
-    else:  # w-only: 88 (MGS-R) / 90 (reflection chains) register chunks of 256 double2
-        assert p["r2e"] == (90 if hh else 88) and p["wt"] == 256
+    else:  # w-only: 89 + 39 (MGS-R) / 90 + 38 (reflection chains) chunks of 256 double2 -- the
+        # whole 4096^2 slab (128 chunks per workgroup) on chip, nothing streamed
+        assert p["r2e"] == (90 if hh else 89) and p["wt"] == 256
+        assert p["nres2"] == N * N // 2, p
 
 
 @pytest.mark.parametrize("R", [2, 4, 8])
