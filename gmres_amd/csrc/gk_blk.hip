@@ -383,6 +383,8 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
             double s = sm[v][0];
 #pragma unroll
             for (int w = 1; w < NW; ++w) s += sm[v][w];
+            if (a.trace != nullptr && t == 0 && xi < RES_TRACE_X)  // (gk_profile_res_trace)
+                a.trace[((i64)blockIdx.x * RES_TRACE_X + xi) * 2] = wall_clock64();
             res_publish_v(a, xi, v, s);
         }
         if (p + 2 < P) {  // the next pass reduces dots: its block's loads overlap this all-gather
@@ -396,6 +398,8 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
                 bc[v] = out;
                 if (!okv) okf = 0;
             }
+            if (a.trace != nullptr && t == 0 && xi < RES_TRACE_X)
+                a.trace[((i64)blockIdx.x * RES_TRACE_X + xi) * 2 + 1] = wall_clock64();
         }
         if (wv < K && lane == 0) atomicAdd(&xdone, 1);
         if constexpr (TCH > 0) {
@@ -755,6 +759,8 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_bla(ResArgs a) {
             double s = sm[wv][0];
 #pragma unroll
             for (int w = 1; w < NW; ++w) s += sm[wv][w];
+            if (a.trace != nullptr && t == 0 && xnow < RES_TRACE_X)  // (gk_profile_res_trace)
+                a.trace[((i64)blockIdx.x * RES_TRACE_X + xnow) * 2] = wall_clock64();
             res_publish_v<4>(a, xnow, wv, s);
         }
         const int xget = nrm ? xnow : xprev;
@@ -767,6 +773,8 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_bla(ResArgs a) {
                 bc[wv] = out;
                 if (!okv) okf = 0;
             }
+            if (a.trace != nullptr && t == 0 && xget < RES_TRACE_X)
+                a.trace[((i64)blockIdx.x * RES_TRACE_X + xget) * 2 + 1] = wall_clock64();
         }
         if (Know > 0) ++xi;
         xprev = xnow;
