@@ -46,7 +46,7 @@ KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res", "prec
 COMM_KINDS = {0: None, 1: "rccl", 2: "local-group", 3: "xgmi-device-exchange"}
 # resident-step variants (gk_res_info / gk_res_plan_query)
 RES_VARIANTS = {0: None, 1: "prefetch", 2: "pairs", 3: "pairs+lds", 4: "w-only", 5: "w+column", 6: "blocked"}
-RES_INFO_KEYS = ["variant", "G", "r2", "l2", "pf", "cw", "wo", "nt", "r2e", "l2e", "lds", "nres2", "la", "cheb_sten", "wt", "blk"]
+RES_INFO_KEYS = ["variant", "G", "r2", "l2", "pf", "cw", "wo", "nt", "r2e", "l2e", "lds", "nres2", "unused12", "cheb_sten", "wt", "blk"]
 
 c_int, c_double, c_ll, c_vp = ctypes.c_int, ctypes.c_double, ctypes.c_longlong, ctypes.c_void_p
 _dp = ctypes.POINTER(ctypes.c_double)

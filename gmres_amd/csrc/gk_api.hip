@@ -134,7 +134,6 @@ struct gk_ctx {
     gk::u64 *res_gath = nullptr;                    // [RES_KMAX values][2][RGMAX][2] all-gather granules
     double *res_gm = nullptr;                       // blocked step: the cycle's Gram table [m+1][RES_SMAX]
     int tune_res_blk = 1;                           // blocked-projection MGS step: S (1 = strict MGS-R)
-    int tune_res_la = 0;                            // ... with one block of look-ahead (k_mgs_bla)
     int watchdog_ms = 0;                            // host watchdog of stream waits (0: from the device deadlines)
     bool broken = false;                            // the watchdog fired: a kernel of this context never completed
     unsigned *hold_word = nullptr, *hold_word_dev = nullptr;  // gk_debug_hold_stream's mapped word
@@ -728,7 +727,6 @@ struct ResPlan {
     bool pc = false;       // column-cache variant (k_mgs_wpc): w in registers, running column cached
     bool pcs = false;      // ... its 16-chunk instantiation (whole column in registers)
     int blk = 0;           // > 1: the blocked-projection MGS step k_mgs_blk with blocks of `blk` (gk_blk.hpp)
-    bool la = false;       // ... its look-ahead build k_mgs_bla
     int bvar = -1;         // ... its instantiation (gk::BLK_*)
     int wt = 0;            // threads per workgroup = double2 per chunk (set by plan_resident)
     i64 nres2 = 0;
@@ -823,7 +821,7 @@ bool wonly_pays(i64 n2, int G) { return wonly_bytes(n2, G) < pairs_bytes(n2, G);
 //   else w and the running column in 2 x 12 registers, plus (GK_TUNE_RES_LDS)
 //   w of 18 more chunks per workgroup in LDS, the rest streamed.
 void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bool hh, bool nt, ResPlan &p,
-                   int tune_pc = -1, int tune_blk = 1, int tune_la = 0) {
+                   int tune_pc = -1, int tune_blk = 1) {
     const i64 n2 = nloc / 2;
     const i64 dcw = gk::RT - 64;
     // small vectors: no more workgroups than two chunks each (a cheaper all-gather)
@@ -866,13 +864,6 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
         p.l2 = g.lx;
         p.lds = (g.lw + tune_blk * (g.lx + g.pfx)) * g.nt * (int)sizeof(double2);
         p.nt = true;
-        if (tune_la && gk::blk_la_supported(var, tune_blk) && gmax <= 512) {
-            // the look-ahead build: no prefetch; the 8-chunk build holds slot set B in LDS
-            p.la = true;
-            p.r2 = g.rw;
-            p.l2 = 0;
-            p.lds = var == gk::BLK_R8 ? 2 * 8 * 512 * (int)sizeof(double2) : 0;
-        }
         return;
     }
     const bool pc_fits = n2 <= (i64)gmax * RES_PC_RW * RES_PC_NT;
@@ -934,16 +925,14 @@ bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
     if (c->tune_res < 0 && c->res_share > 1) return false;
     const int gmax = std::max(1, std::min(gk::RGMAX, c->res_cus / std::max(1, c->res_share)));
     const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : RES_R2_BIG;
-    // (the look-ahead build runs on one rank: the rank-total hop's slots have 2 phases)
     plan_resident(c->nloc, gmax, cap, c->tune_res_lds, c->tune_res_wonly, hh,
-                  c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p, c->tune_res_pc, c->tune_res_blk,
-                  c->tune_res_la && !(collective(c) && c->nranks > 1));
+                  c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p, c->tune_res_pc, c->tune_res_blk);
     if (p.wo && !hh && c->m + 1 > gk::WO_HMAX) return false;  // its H column: WO_HMAX entries of LDS
     return true;
 }
 
 // gk_res_plan_query / gk_res_info layout
-enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, RPI_R2E, RPI_L2E, RPI_LDS, RPI_NRES2, RPI_LA,
+enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, RPI_R2E, RPI_L2E, RPI_LDS, RPI_NRES2, RPI_UNUSED12,
        RPI_CHEB_STEN, RPI_WT, RPI_BLK };
 void plan_info(const ResPlan &p, bool on, long long *info) {
     for (int k = 0; k < GK_RES_INFO_LEN; ++k) info[k] = 0;
@@ -953,7 +942,6 @@ void plan_info(const ResPlan &p, bool on, long long *info) {
                                   : (p.wo ? GK_RES_WONLY
                                           : (p.pf ? GK_RES_PREFETCH : (p.l2 > 0 ? GK_RES_PAIRS_LDS : GK_RES_PAIRS)));
     info[RPI_BLK] = p.blk > 1 ? p.blk : 1;
-    info[RPI_LA] = p.la;
     info[RPI_G] = p.G;
     info[RPI_R2] = p.r2;
     info[RPI_L2] = p.l2;
@@ -1049,7 +1037,7 @@ int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
     if (p.blk > 1) {
         if (a.mode != gk::RES_MGS) return set_err(GK_ERR_STATE, "the blocked step is the MGS-R step's only");
-        const int e = p.la ? gk::blk_launch_la(p.bvar, a, p.G, c->dev, c->st) : gk::blk_launch(p.bvar, p.blk, a, p.G, p.lds, c->dev, c->st);
+        const int e = gk::blk_launch(p.bvar, p.blk, a, p.G, p.lds, c->dev, c->st);
         if (e != 0)
             return set_err(GK_ERR_HIP, "k_mgs_blk (S=%d, variant %d): %s", p.blk, p.bvar,
                            hipGetErrorString(static_cast<hipError_t>(e)));
@@ -2617,7 +2605,11 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
                 return set_err(GK_ERR_ARG, "GK_TUNE_RES_BLOCK %d: blocks of 1 (strict MGS-R), 2 or 4 projections", value);
             c->tune_res_blk = value;
             break;
-        case GK_TUNE_RES_LOOKAHEAD: c->tune_res_la = value != 0; break;
+        case GK_TUNE_RES_LOOKAHEAD:  // (round 5: measured slower than the plain blocked step, removed)
+            if (value != 0)
+                return set_err(GK_ERR_ARG, "GK_TUNE_RES_LOOKAHEAD was removed (look-ahead blocked step measured slower: "
+                                           "profiles/r05/ab_lookahead_r05qr.txt)");
+            break;
         case GK_TUNE_VERR_ORDER: c->tune_verr_order = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:
             if (value < 1) return set_err(GK_ERR_ARG, "timeout must be >= 1 ms");
@@ -2796,12 +2788,11 @@ int gk_sync(gk_ctx *c) {
 }
 
 int gk_res_plan_query(long long nloc, int cus, int share, int hh, int nt, int block, long long *info) {
-    if (info == nullptr || nloc < 2 || cus < 1 || share < 1 || (block != 1 && block != 2 && block != 4 && block != -2))
+    if (info == nullptr || nloc < 2 || cus < 1 || share < 1 || (block != 1 && block != 2 && block != 4))
         return set_err(GK_ERR_ARG, "bad plan query");
     const int gmax = std::max(1, std::min(gk::RGMAX, cus / share));
     ResPlan p;
-    plan_resident(nloc, gmax, RES_R2_BIG, 1, -1, hh != 0, nt < 0 ? nt_auto_for(nloc) : nt != 0, p, -1, block < 0 ? -block : block,
-                  block < 0);
+    plan_resident(nloc, gmax, RES_R2_BIG, 1, -1, hh != 0, nt < 0 ? nt_auto_for(nloc) : nt != 0, p, -1, block);
     plan_info(p, true, info);
     return GK_OK;
 }

@@ -487,398 +487,12 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     }
 }
 
-// --------------------------------------------------------------------------
-// k_mgs_bla: the blocked step with one block of LOOK-AHEAD (GK_TUNE_RES_LOOKAHEAD;
-// S = 2, slabs whose w and two cached blocks fit the registers -- the 1024^2 and
-// 1448^2 (4096^2 / 8) loads).  Pass pi subtracts block sub(pi) = dot(pi - 2) and dots
-// block dot(pi), one block ahead of k_mgs_blk, and the all-gather of those dots is
-// collected at the end of pass pi + 1 -- it overlaps that whole pass instead of
-// following the pass that needs it.  The block subtracted in between (pass pi + 1's,
-// cached on chip as slot set B) enters h by Gram terms:
-//   h_t = z_t - sum_s hB_s <V_{B,s}, V_t> - sum_{s<t} h_s <V_{C,s}, V_t>
-// (MGS in exact arithmetic).  The Gram terms of columns older than the step's newest
-// come from the cycle's table (ResArgs::gm, distances <= 2S - 1 = 3), read into LDS
-// during the pass; those with the newest column are taken in the pass (it is in B or
-// C) and ride the all-gather -- which otherwise carries only the S dots: every value
-// is one more sweep of G partials per workgroup, and the all-gather's latency grows
-// with them (measured: 7 values per all-gather made the step slower than the plain
-// blocked one).  Dots by pass: sweep 1 block i at pass i - 1; none at pass nb1 - 1
-// (sweep 2's first block must see all of sweep 1 subtracted); sweep 2 block i at pass
-// i; none at pass P; the norm at pass P + 1, after the last AXPY.  The cache rotates
-// A <- B <- C every pass (register moves), so sub(pi) is always the block pass pi - 2
-// dotted; DUMMY passes subtract with h = 0.  Schedule and recurrence:
-// tests/lookahead_model.py, checked against strict MGS-R on the CPU
-// (tests/test_lookahead_model.py).  Two all-gathers are in flight, so the granule
-// slots rotate over 4 phases; one rank (the rank-total hop's slots have 2).
-// --------------------------------------------------------------------------
-template <int RW, int S, int WBT, int NT, bool BLDS = false>
-__global__ __launch_bounds__(NT, 1) void k_mgs_bla(ResArgs a) {
-    // BLDS: slot set B in LDS ([S][RW][NT] double2, dynamic) instead of registers -- the
-    // 8-chunk build then keeps a 4-deep batch of loads in flight (with B in registers
-    // only 1 fits beside w and A, and the pass is one memory latency per chunk)
-    extern __shared__ double2 lbs[];
-    constexpr int NW = NT / 64, KM = 3 * S;  // S dots + the newest column's Gram terms with the 2S slots of B, C
-    static_assert(S >= 2 && KM <= RES_KMAX && KM <= NW && 2 * S - 1 < RES_SMAX, "one wave per value; table distances");
-    constexpr int NR = 2 * S;  // table rows read per pass: the columns of A and B
-    __shared__ double sm[KM][NW];
-    __shared__ double bc[KM];
-    __shared__ double hv[S];  // h of the block the NEXT pass subtracts, by slot (0: dummy)
-    __shared__ double gbuf[NR * RES_SMAX];  // table rows of the columns lo .. lo + NR - 1
-    __shared__ int okf;
-    __shared__ double hsh[RHMAX + 1];
-    const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
-    const int j = a.j, cnew = j - 1;  // the newest column (0-based): its Gram terms are taken in the passes
-    const int nb1 = blk_sweep(j, S), P = 2 * nb1, NP = P + 2;
-    auto blk_of = [&](int q) { return q < nb1 ? q : (BLK_REV2 ? 2 * nb1 - 1 - q : q - nb1); };
-    // the sequence index of the block pass pi dots; -1 none, -2 the norm
-    auto dot_of = [&](int pi) {
-        return pi < nb1 - 1 ? pi + 1 : (pi == nb1 - 1 ? -1 : (pi < P ? pi : (pi == P ? -1 : -2)));
-    };
-    // column of slot s of sequence block q (dummy slots: the block's first real column)
-    auto col_of = [&](int q, int s) {
-        const int b = blk_of(q), k = s - (S - blk_n(b, S, j));
-        return blk_lo(b, S) + (k > 0 ? k : 0);
-    };
-    const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
-    const i64 nch = a.nres2 / NT;
-    const i64 c0 = (i64)blockIdx.x * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
-    const double2 *__restrict__ V2 = reinterpret_cast<const double2 *>(a.V);
-    double2 *__restrict__ W2 = reinterpret_cast<double2 *>(a.w);
-    ResClock clk;
-    clk.start(a.stamps);
-    const i64 sstride = (i64)gridDim.x * NT;
-    auto range = [&](int &b, int &e) {  // (opaque: see k_mgs_blk)
-        b = (int)c0;
-        e = (int)cend;
-        asm volatile("" : "+s"(b), "+s"(e));
-    };
-    const unsigned vo = (unsigned)t * 16u;
-    auto at = [&](const double2 *base, int c) {
-        return reinterpret_cast<const double2 *>(reinterpret_cast<const char *>(base + (i64)c * NT) + vo);
-    };
-    auto cols = [&](int q, const double2 *(&X)[S]) {
-#pragma unroll
-        for (int s = 0; s < S; ++s) X[s] = V2 + (i64)col_of(q, s) * ld2;
-    };
-    double2 wr[RW], xa[S][RW], xb[S][BLDS ? 1 : RW];
-    auto bget = [&](int s, int k) -> double2 { return BLDS ? lbs[(s * RW + k) * NT + t] : xb[s][BLDS ? 0 : k]; };
-    auto bput = [&](int s, int k, const double2 &v) {
-        if constexpr (BLDS)
-            lbs[(s * RW + k) * NT + t] = v;
-        else
-            xb[s][k] = v;
-    };
-    {  // w; slot set A = block 0 ({V(:,1)} in slot S-1), B = zeros
-        int cb, ce;
-        range(cb, ce);
-#pragma unroll
-        for (int k = 0; k < RW; ++k) {
-            wr[k] = (cb + k < ce) ? *at(W2, cb + k) : double2{0.0, 0.0};
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                xa[s][k] = double2{0.0, 0.0};
-                bput(s, k, double2{0.0, 0.0});
-            }
-            xa[S - 1][k] = (cb + k < ce) ? ldv<true>(at(V2, cb + k)) : double2{0.0, 0.0};
-        }
-    }
-    double h;
-    {  // h of block 0 = <w, V(:,1)>: the operator launch's partial slab
-        double s = 0.0;
-        for (int k = t; k < a.npin; k += NT) s += a.pin[k];
-        s = wave_sum(s);
-        if (lane == 0) sm[0][wv] = s;
-        __syncthreads();
-        h = sm[0][0];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) h += sm[0][w];
-        __syncthreads();
-    }
-    if (t == 0) {
-#pragma unroll
-        for (int s = 0; s < S - 1; ++s) hv[s] = 0.0;
-        hv[S - 1] = h;
-        if (blockIdx.x == 0) hsh[0] = h;  // H(1, j), first sweep
-    }
-    __syncthreads();
-
-    double acc[KM];
-    int xi = 0, xprev = -1;    // all-gather index of this pass / of the previous pass (-1: none)
-    int gprev = -1;            // the previous pass's newest-column slot in B | C (-1: none)
-    bool ok = true;
-    for (int pi = 0; pi < NP && ok; ++pi) {
-        const int dq = dot_of(pi);
-        const int sq = pi == 0 ? 0 : (pi == 1 ? -1 : dot_of(pi - 2));  // block subtracted (< 0: none)
-        const int bq = pi == 0 ? -1 : dot_of(pi - 1);                   // block cached as B
-        const bool nrm = dq == -2;
-        const double2 *A[S], *B[S], *D[S];
-        cols(sq >= 0 ? sq : 0, A);
-        cols(bq >= 0 ? bq : 0, B);
-        if (dq >= 0)
-            cols(dq, D);
-        else
-#pragma unroll
-            for (int s = 0; s < S; ++s) D[s] = nrm ? A[s] : B[s];  // (values unused: finite columns)
-        // the slot (0..S-1 of B, S..2S-1 of C) holding the newest column, when this pass
-        // dots a block: its Gram terms with every slot of B and C ride the all-gather
-        int gsel = -1;
-        if (dq >= 0) {
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                if (col_of(dq, s) == cnew && s >= S - blk_n(blk_of(dq), S, j)) gsel = S + s;
-                if (bq >= 0 && col_of(bq, s) == cnew && s >= S - blk_n(blk_of(bq), S, j)) gsel = s;
-            }
-        }
-        // table rows for the recurrence after this pass (blocks A and B of this pass are
-        // the previous all-gather's B and C): rows lo .. lo + NR - 1 into gbuf
-        const int glo = (sq >= 0 && bq >= 0) ? min(col_of(sq, 0), col_of(bq, 0)) : 0;
-        if (t < NR * RES_SMAX / 2)  // (rows past the newest column: allocated, finite, unused)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a.gm + (i64)glo * RES_SMAX + 2 * t),
-                                             (lds_void_t *)gbuf, 16, 0, 0);
-        double hc[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) hc[s] = uniform(hv[s]);  // (a DUMMY pass: all 0)
-        double gm0[2 * S];  // 1.0 at the newest column's slot (uniform)
-#pragma unroll
-        for (int s = 0; s < 2 * S; ++s) gm0[s] = gsel == s ? 1.0 : 0.0;
-#pragma unroll
-        for (int e = 0; e < KM; ++e) acc[e] = 0.0;
-        // the closing reductions of one element pair of w (after the AXPYs): the dots with
-        // block C -- or ||w||^2 into acc[0] -- and the newest column's Gram terms with the
-        // 2S slots of B and C (a uniform select picks the newest column's vector)
-        auto red = [&](const double2 &x, const double2 (&b)[S], const double2 (&c)[S]) {
-            const double2 y0 = nrm ? x : c[0];
-            acc[0] = acc[0] + x.x * y0.x;
-            acc[0] = acc[0] + x.y * y0.y;
-#pragma unroll
-            for (int d = 1; d < S; ++d) {
-                acc[d] = acc[d] + x.x * c[d].x;
-                acc[d] = acc[d] + x.y * c[d].y;
-            }
-            if (gsel >= 0) {  // (uniform) the newest column's vector by 0 / 1 masks: a select of
-                              // the slot arrays became a dynamically indexed scratch array
-                double2 nv{0.0, 0.0};
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    nv.x = nv.x + b[s].x * gm0[s];
-                    nv.y = nv.y + b[s].y * gm0[s];
-                    nv.x = nv.x + c[s].x * gm0[S + s];
-                    nv.y = nv.y + c[s].y * gm0[S + s];
-                }
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    acc[S + s] = acc[S + s] + b[s].x * nv.x;
-                    acc[S + s] = acc[S + s] + b[s].y * nv.y;
-                    acc[2 * S + s] = acc[2 * S + s] + c[s].x * nv.x;
-                    acc[2 * S + s] = acc[2 * S + s] + c[s].y * nv.y;
-                }
-            }
-        };
-        {
-            int cb, ce;
-            range(cb, ce);
-#pragma unroll
-            for (int k0 = 0; k0 < RW; k0 += WBT) {
-                double2 bv[WBT][S];
-#pragma unroll
-                for (int u = 0; u < WBT; ++u) {
-                    const int k = k0 + u;
-                    if (k < RW && cb + k < ce) {
-#pragma unroll
-                        for (int d = 0; d < S; ++d) bv[u][d] = ldv<false>(at(D[d], cb + k));
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < WBT; ++u) {
-                    const int k = k0 + u;
-                    if (k < RW && cb + k < ce) {
-#pragma unroll
-                        for (int s = 0; s < S; ++s) {
-                            wr[k].x = wr[k].x - hc[s] * xa[s][k].x;
-                            wr[k].y = wr[k].y - hc[s] * xa[s][k].y;
-                        }
-                        double2 bb[S];
-#pragma unroll
-                        for (int s = 0; s < S; ++s) bb[s] = bget(s, k);
-                        red(wr[k], bb, bv[u]);
-#pragma unroll
-                        for (int s = 0; s < S; ++s) {  // rotate: A <- B <- C
-                            xa[s][k] = bb[s];
-                            bput(s, k, bv[u][s]);
-                        }
-                    }
-                }
-            }
-        }
-        // streamed part: w and every column from HBM, one element pair at a time
-        for (i64 e = a.nres2 + (i64)blockIdx.x * NT + t; e < n2; e += sstride) {
-            double2 x = W2[e], bb[S], cc[S];
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                const double2 v = ldv<true>(A[s] + e);
-                x.x = x.x - hc[s] * v.x;
-                x.y = x.y - hc[s] * v.y;
-            }
-            W2[e] = x;
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                bb[s] = ldv<false>(B[s] + e);
-                cc[s] = ldv<false>(D[s] + e);
-            }
-            red(x, bb, cc);
-        }
-        if ((a.n & 1) && blockIdx.x == 0 && t == 0) {  // odd-length tail element
-            const i64 e = a.n - 1;
-            double x = a.w[e];
-#pragma unroll
-            for (int s = 0; s < S; ++s) x = x - hc[s] * reinterpret_cast<const double *>(A[s])[e];
-            a.w[e] = x;
-            double2 bb[S], cc[S];
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                bb[s] = double2{reinterpret_cast<const double *>(B[s])[e], 0.0};
-                cc[s] = double2{reinterpret_cast<const double *>(D[s])[e], 0.0};
-            }
-            red(double2{x, 0.0}, bb, cc);
-        }
-        clk.passed(a.stamps);
-        // publish this pass's values (all-gather xi), collect the previous pass's (xprev);
-        // the norm's is collected at once
-        const int Know = nrm ? 1 : (dq >= 0 ? (gsel >= 0 ? KM : S) : 0);
-        const int Kprev = xprev >= 0 ? (gprev >= 0 ? KM : S) : 0;
-#pragma unroll
-        for (int e = 0; e < KM; ++e)
-            if (e < Know) {
-                const double r = wave_sum(acc[e]);
-                if (lane == 0) sm[e][wv] = r;
-            }
-        if (t == 0) okf = 1;
-        __syncthreads();
-        const int xnow = Know > 0 ? xi : -1;
-        if (wv < Know) {
-            double s = sm[wv][0];
-#pragma unroll
-            for (int w = 1; w < NW; ++w) s += sm[wv][w];
-            if (a.trace != nullptr && t == 0 && xnow < RES_TRACE_X)  // (gk_profile_res_trace)
-                a.trace[((i64)blockIdx.x * RES_TRACE_X + xnow) * 2] = wall_clock64();
-            res_publish_v<4>(a, xnow, wv, s);
-        }
-        const int xget = nrm ? xnow : xprev;
-        const int Kget = nrm ? 1 : Kprev;
-        const int ggot = gprev;  // the newest-column slot of the collected all-gather
-        if (wv < Kget) {
-            double out = 0.0;
-            const bool okv = res_collect_v<BLK_POLL_SLEEP, 4>(a, xget, wv, &out);
-            if (lane == 0) {
-                bc[wv] = out;
-                if (!okv) okf = 0;
-            }
-            if (a.trace != nullptr && t == 0 && xget < RES_TRACE_X)
-                a.trace[((i64)blockIdx.x * RES_TRACE_X + xget) * 2 + 1] = wall_clock64();
-        }
-        if (Know > 0) ++xi;
-        xprev = xnow;
-        gprev = gsel;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's table rows landed too)
-        __syncthreads();
-        clk.waited(a.stamps);
-        ok = okf != 0;
-        if (!ok || nrm) break;
-        // h of the block the next pass subtracts (bq = dot_of(pi - 1), collected now),
-        // corrected for the block this pass subtracted (sq, with hc) and within itself
-        if (t == 0) {
-            double hn[S];
-#pragma unroll
-            for (int s = 0; s < S; ++s) hn[s] = 0.0;
-            if (Kget > 0 && bq >= 0) {
-                const int r = blk_n(blk_of(bq), S, j);
-                // Gram term of slot s of block `sq` (y = 0) or of block `bq` (y = 1) with slot d of bq:
-                // the newest column's from the all-gather (slots of that pass: B = sq, C = bq), the
-                // others from the table (0 past its reach: those terms multiply an h of 0)
-                auto gram = [&](int y, int s, int d) -> double {
-                    const int qa = y == 0 ? (sq >= 0 ? sq : 0) : bq;
-                    const int ca = col_of(qa, s), cd = col_of(bq, d);
-                    if (ggot >= 0 && (ca == cnew || cd == cnew)) {
-                        const int other = ca == cnew ? S + d : (y == 0 ? s : S + s);
-                        return bc[S + other];
-                    }
-                    const int hi = ca > cd ? ca : cd, dist = ca > cd ? ca - cd : cd - ca;
-                    if (dist == 0 || dist >= RES_SMAX || hi - glo < 0 || hi - glo >= NR) return 0.0;
-                    return gbuf[(hi - glo) * RES_SMAX + dist];
-                };
-#pragma unroll
-                for (int d = 0; d < S; ++d)
-                    if (d >= S - r) {
-                        double hk = bc[d];
-#pragma unroll
-                        for (int s = 0; s < S; ++s) hk = hk - hc[s] * gram(0, s, d);
-#pragma unroll
-                        for (int s = 0; s < d; ++s) hk = hk - hn[s] * gram(1, s, d);
-                        hn[d] = hk;
-                    }
-                if (blockIdx.x == 0) {
-                    const bool sw1 = bq < nb1;
-                    const int lo = blk_lo(blk_of(bq), S);
-#pragma unroll
-                    for (int d = 0; d < S; ++d)
-                        if (d >= S - r) {
-                            const int c = lo + d - (S - r);
-                            hsh[c] = (sw1 ? 0.0 : hsh[c]) + hn[d];
-                        }
-                    // the newest column's table row, once per cycle (sweep 1: its block was dotted
-                    // with the block before it in B): gm[cnew][dist] = <V(cnew - dist), V(cnew)>
-                    if (sw1 && ggot >= S) {
-#pragma unroll
-                        for (int s = 0; s < 2 * S; ++s) {
-                            const int c = s < S ? (sq >= 0 ? col_of(sq, s) : -1) : col_of(bq, s - S);
-                            const int dist = cnew - c;
-                            if (c >= 0 && dist > 0 && dist < RES_SMAX) a.gm[(i64)cnew * RES_SMAX + dist] = bc[S + s];
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < S; ++s) hv[s] = hn[s];
-        }
-        __syncthreads();
-    }
-    if (!ok) return;  // uniform per workgroup; *err is set
-    const double hn = sqrt(bc[0]);
-    double2 *__restrict__ O2 = reinterpret_cast<double2 *>(a.vout);
-    auto outv = [&](const double2 &v) { return hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0}; };
-    {
-        int cb, ce;
-        range(cb, ce);
-#pragma unroll
-        for (int k = 0; k < RW; ++k)
-            if (cb + k < ce) O2[(i64)(cb + k) * NT + t] = outv(wr[k]);
-    }
-    for (i64 e = a.nres2 + (i64)blockIdx.x * NT + t; e < n2; e += sstride) O2[e] = outv(W2[e]);
-    if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
-    clk.finish(a.stamps, RES_MGS);
-    if (blockIdx.x == 0) {
-        __syncthreads();
-        for (int k = t; k < j; k += NT) {
-            a.hs[k] = hsh[k];
-            a.hcopy[k] = hsh[k];
-        }
-        if (t == 0) {
-            a.hs[j] = hn;
-            a.hcopy[j] = hn;
-        }
-    }
-}
-
 // ------------------------------------------------------------------ host ---
 #ifndef GK_BLK_KERNEL_ONLY  // (register-budget experiments instantiate one kernel themselves)
 #ifndef GK_BLK_TOUCH
 #define GK_BLK_TOUCH 28
 #endif
 constexpr int BLK_TOUCH = GK_BLK_TOUCH;  // the w-only build's touched chunks (k_mgs_wres's TOUCH_MGS)
-#ifndef GK_BLK_LA_WB8
-#define GK_BLK_LA_WB8 4
-#endif
-constexpr int BLK_LA_WB8 = GK_BLK_LA_WB8;  // the look-ahead 8-chunk build's batch
 
 namespace {
 
@@ -941,31 +555,6 @@ BlkGeom blk_geom(int var, int S) {
 int blk_variant(long long chunks512) {
     return chunks512 <= 4 ? BLK_R4 : chunks512 <= 8 ? BLK_R8 : chunks512 <= 16 ? BLK_R16 : chunks512 <= 32 ? BLK_R32 : BLK_WONLY;
 }
-
-int blk_launch_la(int var, const ResArgs &a, int G, int dev, hipStream_t st) {
-    if (G > 512) return (int)hipErrorInvalidValue;  // 4 granule phases per replica
-    switch (var) {
-        case BLK_R4: k_mgs_bla<4, 2, 4, 512><<<G, 512, 0, st>>>(a); break;
-        case BLK_R8: {
-            constexpr int lds = 2 * 8 * 512 * (int)sizeof(double2);  // slot set B in LDS
-            auto kern = &k_mgs_bla<8, 2, BLK_LA_WB8, 512, true>;
-            static std::atomic<int> attr[64];
-            if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
-            if (attr[dev].load() < lds) {
-                const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-                if (e != hipSuccess) return (int)e;
-                attr[dev] = lds;
-            }
-            kern<<<G, 512, lds, st>>>(a);
-            break;
-        }
-        default: return (int)hipErrorInvalidValue;
-    }
-    return (int)hipGetLastError();
-}
-
-bool blk_la_supported(int var, int S) { return S == 2 && (var == BLK_R4 || var == BLK_R8); }
 
 int blk_launch(int var, int S, const ResArgs &a, int G, int lds, int dev, hipStream_t st) {
     switch (S) {

@@ -45,9 +45,5 @@ int blk_variant(long long chunks512);  // chunks per thread at 512 threads; BLK_
 // `lds` bytes of dynamic LDS; returns a hipError_t (hipErrorInvalidValue for an
 // unsupported S / variant).
 int blk_launch(int var, int S, const ResArgs &a, int G, int lds, int dev, hipStream_t st);
-// The look-ahead build (k_mgs_bla, GK_TUNE_RES_LOOKAHEAD): S = 2, the 4- and 8-chunk
-// variants (w and two cached blocks in registers), one rank, G <= 512.
-bool blk_la_supported(int var, int S);
-int blk_launch_la(int var, const ResArgs &a, int G, int dev, hipStream_t st);
 
 }  // namespace gk

@@ -53,6 +53,14 @@ __device__ __forceinline__ double2 ldv(const double2 *p) {
     }
 }
 
+// A plain (default-policy) load through an address-space-1 pointer: where the compiler
+// cannot prove a pointer global (pointers selected per pass from small arrays) it emits
+// FLAT loads, and waited for each before issuing the next inside an unrolled batch.
+__device__ __forceinline__ double2 ldg(const double2 *p) {
+    const d2v t = *(const __attribute__((address_space(1))) d2v *)p;
+    return double2{t.x, t.y};
+}
+
 // Fused reductions of a pass: none, <y, vdot>, or <y, y>.
 enum { ACC_NONE = 0, ACC_DOT = 1, ACC_NORM = 2 };
 

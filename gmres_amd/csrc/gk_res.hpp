@@ -470,20 +470,16 @@ __device__ __forceinline__ void res_exchange(const ResArgs &a, int p, const doub
 constexpr int RES_SMAX = 4;                    // largest block of projections
 constexpr int RES_KMAX = 2 * RES_SMAX - 1;     // its dots + the Gram terms of its newest column
 constexpr i64 RES_GATH_ALL = (i64)RES_KMAX * RES_GATH_WORDS;
-static_assert(RES_NREP > 1 && RES_REP_STRIDE >= 4 * 512 * 2, "4 granule phases of 512 workgroups fit a replica");
 static_assert(RES_KMAX <= XS_REP_STEP, "the values of one exchange must fit a replica's value slots");
 
 // One wave: publish value v of exchange p (s = this workgroup's partial of it) --
-// its granule pair into every replica, no wait.  PH: granule phases of a replica (2;
-// 4 when two exchanges are in flight -- the look-ahead step, G <= 512 -- since a
-// workgroup may then publish exchange p + 2 while a slower one still sweeps p).
-template <int PH = 2>
+// its granule pair into every replica, no wait.
 __device__ __forceinline__ void res_publish_v(const ResArgs &a, int p, int v, double s) {
     const int lane = threadIdx.x & 63;
     const unsigned tag = a.tag0 + (unsigned)p;
     if (lane < 2 * RES_NREP) {
         u64 *gv = a.gath + (i64)v * RES_GATH_WORDS;
-        u64 *q = gv + (RES_NREP > 1 ? RES_REP0 + (lane >> 1) * RES_REP_STRIDE : 0) + (i64)(p % PH) * gridDim.x * 2;
+        u64 *q = gv + (RES_NREP > 1 ? RES_REP0 + (lane >> 1) * RES_REP_STRIDE : 0) + (i64)(p & 1) * gridDim.x * 2;
         const u64 bits = (u64)__double_as_longlong(s);
         const int half = lane & 1;
         __hip_atomic_store(q + 2 * blockIdx.x + half, ((u64)tag << 32) | (half ? (unsigned)(bits >> 32) : (unsigned)bits),
@@ -495,13 +491,13 @@ __device__ __forceinline__ void res_publish_v(const ResArgs &a, int p, int v, do
 // copy (replica blockIdx % NREP; on N ranks the pushers only, then the rank-total
 // hop).  Returns false when a deadline passed (*a.err set); *out = the grid (and
 // rank) total, the same bits in every workgroup and on every rank.
-template <int SLEEP, int PH = 2>
+template <int SLEEP>
 __device__ __forceinline__ bool res_collect_v(const ResArgs &a, int p, int v, double *out) {
     const int lane = threadIdx.x & 63;
     const int G = gridDim.x;
     const unsigned tag = a.tag0 + (unsigned)p;
     const u64 *slot = a.gath + (i64)v * RES_GATH_WORDS +
-                      (RES_NREP > 1 ? RES_REP0 + (int)(blockIdx.x % RES_NREP) * RES_REP_STRIDE : 0) + (i64)(p % PH) * G * 2;
+                      (RES_NREP > 1 ? RES_REP0 + (int)(blockIdx.x % RES_NREP) * RES_REP_STRIDE : 0) + (i64)(p & 1) * G * 2;
     const u64 deadline = wall_clock64() + a.timeout;
     double acc = 0.0;
     bool all_ok = true;

@@ -289,7 +289,7 @@ int gk_sync(gk_ctx *ctx);
  * info[GK_RES_INFO_LEN]: variant, workgroups G, R2, L2, prefetch, control
  * wave, w-only, non-temporal column loads, register / LDS chunks per
  * workgroup in use, dynamic LDS bytes, resident double2 of the slab, and
- * whether the blocked step runs its look-ahead build (la),
+ * (unused, 0),
  * (gk_res_info only) whether the Arnoldi step's Chebyshev(k) pass forms z = A v in its own
  * stage 0 (1 / 0; -1 on a multi-rank context whose smallest slab is not known
  * until its first solve), the threads per workgroup (= double2 per chunk), and the
@@ -297,8 +297,7 @@ int gk_sync(gk_ctx *ctx);
  * gk_res_plan_query: pure host computation for a slab of nloc unknowns on a
  * device with `cus` compute units shared by `share` contexts; hh != 0 the
  * reflection chains' plan; nt: -1 auto (from nloc), 0 / 1 forced; block: the
- * GK_TUNE_RES_BLOCK value (1, 2 or 4) of the MGS step's plan, -2 for S = 2 with
- * GK_TUNE_RES_LOOKAHEAD.  No device
+ * GK_TUNE_RES_BLOCK value (1, 2 or 4) of the MGS step's plan.  No device
  * is touched (the CPU tests pin every production split with it).
  * gk_res_info: the plan this context uses now (its tuning, communicator and
  * sharing applied); variant GK_RES_NONE when steps run launch by launch. */
@@ -390,13 +389,9 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          instead of 2j.  Not bit-identical to the strict step (within the
  *                          residual-history tolerance of DESIGN.md 4.3).  MGS-R resident
  *                          steps only; Householder and the launch path stay strict.
- *   GK_TUNE_RES_LOOKAHEAD  0 (default); 1 with GK_TUNE_RES_BLOCK 2 on one rank: the blocked
- *                          step's look-ahead build k_mgs_bla for slabs of <= 8 chunks of 512
- *                          double2 per workgroup (1024^2, 4096^2 / 8): each pass dots the
- *                          block AFTER the next one and its all-gather is collected a pass
- *                          later, overlapping that pass; the block subtracted in between
- *                          enters h by Gram terms taken with the dots.  Elsewhere the plain
- *                          blocked step runs (gk_res_info "la" says which)
+ *   GK_TUNE_RES_LOOKAHEAD  removed in round 5 (a look-ahead build of the blocked step: parity
+ *                          green, measured slower than the plain one -- DESIGN.md 3.1c); 1 is
+ *                          refused
  *   GK_TUNE_WATCHDOG_MS    limit of every host wait on the context's stream (gk_sync, the step
  *                          waits, gk_update_x ...); 0 (default) = twice the longest device
  *                          deadline plus a minute.  Past it the wait returns GK_ERR_COMM (a

@@ -1,7 +1,10 @@
-"""Host model of the look-ahead blocked MGS-R step (k_mgs_bla, gk_blk.hip): the
-pass schedule and the h recurrence the kernel runs, in numpy, so that the
-schedule's invariants and its agreement with strict MGS-R
-(gmres_mgsr.f90:341-360) are checked on the CPU (tests/test_lookahead_model.py).
+"""Host model of a look-ahead blocked MGS-R step: the pass schedule and the h
+recurrence, in numpy, checked against strict MGS-R (gmres_mgsr.f90:341-360) on
+the CPU (tests/test_lookahead_model.py).  Round 5 built it as a kernel
+(k_mgs_bla) on this model -- parity green against the reference's histories --
+and removed it: every build measured slower than the plain blocked step
+(profiles/r05/ab_lookahead_r05mnop.txt, ab_lookahead_r05qr.txt).
+The model stays as the tested specification for a next attempt.
 
 The blocked step dots block b in the pass that subtracts block
 b-1 and all-gathers right after it; the look-ahead step dots block b one pass

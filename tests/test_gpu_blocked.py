@@ -30,24 +30,23 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REF = json.load(open(os.path.join(HERE, "golden", "reference_runs.json")))
 
 
-def _tune(c, S, share=1, la=False):
+def _tune(c, S, share=1):
     from gmres_amd import _native as nat
 
     c.tune(nat.GK_TUNE_RES_BLOCK, S)
-    c.tune(nat.GK_TUNE_RES_LOOKAHEAD, int(la))
     if share > 1:
         c.tune(nat.GK_TUNE_RES, 1)
         c.tune(nat.GK_TUNE_RES_SHARE, share)
     c.tune(nat.GK_TUNE_RES_TIMEOUT_MS, 10000)
 
 
-def _run(N, m, S, cycles, share=1, prec="identity", tol=1e-15, want_x=False, la=False):
+def _run(N, m, S, cycles, share=1, prec="identity", tol=1e-15, want_x=False):
     import gmres_amd as ga
 
     with ga.Context(N, m) as c:
         c.set_precond(prec, (8.2, 0.2), 8)
         c.set_rhs_ones()
-        _tune(c, S, share, la)
+        _tune(c, S, share)
         plan = c.res_info()
         c.profile(True)
         c.profile_reset()
@@ -208,62 +207,6 @@ def test_blocked_knob_rejects_other_sizes():
         c.tune(nat.GK_TUNE_RES_BLOCK, 2)
         assert c.res_info()["blk"] == 2
         assert c.res_info(hh=True)["blk"] == 1  # the reflection chains stay strict
+        with pytest.raises(Exception, match="removed"):  # the look-ahead build (round 5, measured slower)
+            c.tune(nat.GK_TUNE_RES_LOOKAHEAD, 1)
 
-
-# ---------------------------------------------------------------- look-ahead ---
-# k_mgs_bla (GK_TUNE_RES_LOOKAHEAD with S = 2): each pass dots the block after the
-# next one and collects that all-gather a pass later; the schedule and recurrence are
-# the host model's (tests/lookahead_model.py, checked against strict MGS-R on the CPU).
-
-
-@pytest.mark.parametrize("share,chunks", [(1, 4), (2, 8)])
-def test_lookahead_1024_vs_reference(share, chunks):
-    """Both look-ahead builds (4 and 8 register chunks: the 1024^2 and 4096^2 / 8
-    loads) on the 1024^2 slab against the reference's twelve-cycle history."""
-    g = REF["mgsr_omp_identity_1024_m95_12cyc_t8"]["hist_res"]
-    r, plan, prof = _run(1024, 95, 2, 12, share=share, la=True)
-    assert plan["variant"] == "blocked" and plan["blk"] == 2 and plan["la"] == 1 and plan["r2e"] == chunks, plan
-    assert prof["res"][1] >= 95 * 12 and prof["proj"][1] <= 1, prof
-    print(f"\n[look-ahead share={share}] 1024^2 12 cycles: max rel dev vs reference {_dev(r.hist_res, g):.2e}")
-    _contract(r.hist_res, g)
-
-
-def test_lookahead_1448_cycle_vs_reference():
-    """The 8-GPU per-GPU load (1448^2: 8 chunks per thread, a streamed remainder and
-    an even n) against the reference's own 1448^2 cycle."""
-    g = REF["mgsr_omp_identity_1448_m95_1cyc_t8"]
-    r, plan, _ = _run(1448, 95, 2, 1, la=True)
-    assert plan["la"] == 1 and plan["r2e"] == 8, plan
-    print(f"\n[look-ahead] 1448^2 cycle 1: rel dev vs reference {_dev(r.hist_res, g['hist_res']):.2e}")
-    assert r.hist_res[0] == pytest.approx(g["hist_res"][0], rel=1e-9)  # (a cut run records no final_err)
-
-
-def test_lookahead_128_converges_like_reference():
-    g = REF["mgsr_omp_identity_128_m30"]
-    r, plan, _ = _run(128, 30, 2, 1000, want_x=True, la=True)
-    assert plan["la"] == 1, plan
-    print(f"\n[look-ahead] 128^2: {r.iterations} iterations (reference {g['iterations']})")
-    assert abs(r.iterations - g["iterations"]) <= 0.01 * g["iterations"]
-    assert r.final_err[r.n_out - 1] < 1e-15
-    assert np.max(np.abs(r.x - 1.0)) < 1e-9
-    hi = [k for k, v in enumerate(g["hist_res"]) if v > 1e-10]
-    _contract(r.hist_res[: len(hi)], g["hist_res"][: len(hi)])
-
-
-@pytest.mark.parametrize("N,m", [(127, 30), (100, 20), (96, 7)])
-def test_lookahead_ragged_slabs_vs_oracle(oracle, N, m):
-    """Odd n, partial chunks and blocks shorter than S at every step (m = 7: the
-    sweeps' boundary passes at every j) against the oracle, ten cycles."""
-    r, plan, _ = _run(N, m, 2, 10, la=True)
-    assert plan["la"] == 1, plan
-    ref = oracle.gmres_mgsr(oracle.rhs_ones(N), N, m, variant=oracle.MGSR_OMP, max_cycles=10)
-    print(f"\n[look-ahead] {N}^2 m={m}: max rel dev vs oracle {_dev(r.hist_res, ref.hist_res):.2e}")
-    _contract(r.hist_res, ref.hist_res)
-
-
-def test_lookahead_falls_back_where_unsupported():
-    """Slabs past 8 chunks per thread (and S = 4) run the plain blocked build."""
-    r, plan, _ = _run(1024, 95, 2, 1, share=4, la=True)
-    assert plan["la"] == 0 and plan["variant"] == "blocked", plan
-    r4, plan4, _ = _run(1024, 95, 4, 1, la=True)
-    assert plan4["la"] == 0 and plan4["blk"] == 4, plan4

@@ -111,16 +111,3 @@ def test_blocked_plan_rejects_other_blocks():
     buf = (_native.c_ll * len(_native.RES_INFO_KEYS))()
     assert _native.hip().gk_res_plan_query(1 << 20, 256, 1, 0, -1, 3, buf) == -1
 
-
-@pytest.mark.parametrize("N,R,la", [(1024, 1, 1), (4096, 8, 1), (4096, 4, 0), (4096, 1, 0)])
-def test_lookahead_plan(N, R, la):
-    """GK_TUNE_RES_LOOKAHEAD (block -2 in the query): the look-ahead build where w
-    and two cached blocks fit the registers (<= 8 chunks per thread), else the
-    plain blocked build."""
-    nl = max(n for _, n in ga.slab_partition(N, R))
-    p = ga.res_plan_query(N * nl, 256, 1, False, -1, block=-2)
-    assert p["variant"] == "blocked" and p["blk"] == 2 and p["la"] == la, p
-    if la:
-        assert p["lds"] == (2 * 8 * 512 * 16 if p["r2e"] == 8 else 0) and p["r2"] == p["r2e"] and p["wt"] == 512, p
-    q = ga.res_plan_query(N * nl, 256, 1, False, -1, block=2)
-    assert q["la"] == 0
