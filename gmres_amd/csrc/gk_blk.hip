@@ -509,10 +509,19 @@ struct BlkCfg<2> {
     static constexpr int wb[BLK_NVAR] = {4, 4, 4, 2, 4};
 };
 template <>
+#ifndef GK_BLK_S4_R8_1W
+#define GK_BLK_S4_R8_1W 1
+#endif
+// S = 4 at <= 8 chunks of 512 (the 4096^2 / 8 load): one wave per SIMD -- 16 chunks of w and
+// of each of the 4 cached columns in ~450 registers -- so that LDS is free for the first 8
+// chunks of the next dot block, prefetched during the all-gather (the two-wave build had no
+// room for either prefetch or cache: 4.32 -> 4.12 us per projection at 1448^2,
+// profiles/r05/ab_blk_s4_onewave_r05t.txt)
 struct BlkCfg<4> {
-    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4}, {8, 0, 8, 0, 512, 0}, {16, 0, 2, 4, 512, 0},
-                                            {32, 0, 0, 4, 512, 0}, {88, 38, 0, 0, 256, 0}};
-    static constexpr int wb[BLK_NVAR] = {4, 2, 2, 1, 2};
+    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4},
+                                            GK_BLK_S4_R8_1W ? BlkGeom{16, 0, 16, 0, 256, 8} : BlkGeom{8, 0, 8, 0, 512, 0},
+                                            {16, 0, 2, 4, 512, 0}, {32, 0, 0, 4, 512, 0}, {88, 38, 0, 0, 256, 0}};
+    static constexpr int wb[BLK_NVAR] = {4, GK_BLK_S4_R8_1W ? 4 : 2, 2, 1, 2};
 };
 
 template <int S, int V>

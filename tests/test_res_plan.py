@@ -81,7 +81,7 @@ BLOCKED = [
     (8192, 8, 2, (512, 32, 0, 1, 9)),
     (4096, 1, 2, (256, 90, 38, 0, 0)),
     (1024, 1, 4, (512, 4, 0, 4, 0)),
-    (4096, 8, 4, (512, 8, 0, 8, 0)),
+    (4096, 8, 4, (256, 16, 0, 16, 0)),  # one wave per SIMD: LDS left for the prefetch
     (4096, 4, 4, (512, 16, 0, 2, 4)),
     (4096, 2, 4, (512, 32, 0, 0, 4)),
     (4096, 1, 4, (256, 88, 38, 0, 0)),
@@ -94,8 +94,8 @@ def test_blocked_plan_of_every_split(N, R, S, want):
     p = ga.res_plan_query(N * nl, 256, 1, False, -1, block=S)
     assert p["variant"] == "blocked" and p["blk"] == S and p["G"] == 256, p
     assert (p["wt"], p["r2e"], p["l2e"], p["r2"], p["l2"]) == want, p
-    lw = 38 if p["wt"] == 256 else 0
-    pfx = {(512, 4): 4, (512, 8): 8 if S == 2 else 0}.get((p["wt"], p["r2e"]), 0)  # LDS prefetch of small slabs
+    lw = 38 if p["wt"] == 256 and p["r2e"] > 32 else 0  # (the w-only build; not the one-wave S = 4 one)
+    pfx = {(512, 4): 4, (512, 8): 8, (256, 16): 8}.get((p["wt"], p["r2e"]), 0)  # LDS prefetch of small slabs
     assert p["lds"] == (lw + S * (p["l2"] + pfx)) * p["wt"] * 16 and p["lds"] + 5 * 1024 <= 160 * 1024, p
     # the whole slab is resident except the w-only S = 4 build's two streamed chunks
     assert p["nres2"] <= N * nl // 2
