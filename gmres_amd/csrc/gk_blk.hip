@@ -502,13 +502,15 @@ template <int S>
 struct BlkCfg;
 // (measured in the compile: the largest spill-free geometry of each variant; a
 // deeper batch or more cached register chunks spilled)
+// (S = 2 at 16 chunks as a one-wave build -- the whole slab and both columns in registers, half
+// the next dot block prefetched -- was slower: 2048^2 8.04 -> 8.84 us per projection, its
+// all-gather wait 2.1 -> 3.2 us; profiles/r05/ab_blk_s2_onewave_r05v.txt)
 template <>
 struct BlkCfg<2> {
     static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4}, {8, 0, 8, 0, 512, 8}, {16, 0, 7, 9, 512, 0},
                                             {32, 0, 1, 9, 512, 0}, {90, 38, 0, 0, 256, 0}};
     static constexpr int wb[BLK_NVAR] = {4, 4, 4, 2, 4};
 };
-template <>
 #ifndef GK_BLK_S4_R8_1W
 #define GK_BLK_S4_R8_1W 1
 #endif
@@ -517,6 +519,7 @@ template <>
 // chunks of the next dot block, prefetched during the all-gather (the two-wave build had no
 // room for either prefetch or cache: 4.32 -> 4.12 us per projection at 1448^2,
 // profiles/r05/ab_blk_s4_onewave_r05t.txt)
+template <>
 struct BlkCfg<4> {
     static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4},
                                             GK_BLK_S4_R8_1W ? BlkGeom{16, 0, 16, 0, 256, 8} : BlkGeom{8, 0, 8, 0, 512, 0},
