@@ -39,6 +39,7 @@ GK_TUNE_RES_BLOCK = 23
 GK_TUNE_WATCHDOG_MS = 24
 GK_TUNE_HH_NORM_ORDER = 25
 GK_TUNE_RES_LOOKAHEAD = 26
+GK_TUNE_RES_PF = 27
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 (GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES, GK_KID_PREC,
  GK_KID_HALO, GK_KID_GRAPH) = range(10)

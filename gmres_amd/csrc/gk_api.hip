@@ -134,6 +134,7 @@ struct gk_ctx {
     gk::u64 *res_gath = nullptr;                    // [RES_KMAX values][2][RGMAX][2] all-gather granules
     double *res_gm = nullptr;                       // blocked step: the cycle's Gram table [m+1][RES_SMAX]
     int tune_res_blk = 1;                           // blocked-projection MGS step: S (1 = strict MGS-R)
+    int tune_res_pf = -1;                           // strict MGS step on the blocked kernel's LDS prefetch (S = 1)
     int watchdog_ms = 0;                            // host watchdog of stream waits (0: from the device deadlines)
     bool broken = false;                            // the watchdog fired: a kernel of this context never completed
     unsigned *hold_word = nullptr, *hold_word_dev = nullptr;  // gk_debug_hold_stream's mapped word
@@ -726,7 +727,8 @@ struct ResPlan {
     bool pf = false, nt = false, cw = false, wo = false;
     bool pc = false;       // column-cache variant (k_mgs_wpc): w in registers, running column cached
     bool pcs = false;      // ... its 16-chunk instantiation (whole column in registers)
-    int blk = 0;           // > 1: the blocked-projection MGS step k_mgs_blk with blocks of `blk` (gk_blk.hpp)
+    int blk = 0;           // > 1: the blocked-projection MGS step k_mgs_blk with blocks of `blk` (gk_blk.hpp);
+                           // 1 with bvar >= 0: the strict step on k_mgs_blk<S = 1> (GK_TUNE_RES_PF)
     int bvar = -1;         // ... its instantiation (gk::BLK_*)
     int wt = 0;            // threads per workgroup = double2 per chunk (set by plan_resident)
     i64 nres2 = 0;
@@ -821,7 +823,7 @@ bool wonly_pays(i64 n2, int G) { return wonly_bytes(n2, G) < pairs_bytes(n2, G);
 //   else w and the running column in 2 x 12 registers, plus (GK_TUNE_RES_LDS)
 //   w of 18 more chunks per workgroup in LDS, the rest streamed.
 void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bool hh, bool nt, ResPlan &p,
-                   int tune_pc = -1, int tune_blk = 1) {
+                   int tune_pc = -1, int tune_blk = 1, int tune_pf = -1) {
     const i64 n2 = nloc / 2;
     const i64 dcw = gk::RT - 64;
     // small vectors: no more workgroups than two chunks each (a cheaper all-gather)
@@ -849,12 +851,21 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
     // profiles/r04/ab_pc512_r04j.jsonl).  The one-wave build streamed at ~4.7 TB/s
     // to k_mgs_res's ~6.8, so there it had to save a third of the bytes (2048^2 was
     // slower on it: 11.3-11.5 vs 9.6 us, ab_wpc_touch_r04e).
-    if (!hh && tune_blk > 1) {
+    const int var = gk::blk_variant((n2 + (i64)gmax * 512 - 1) / ((i64)gmax * 512));
+    // The strict step on k_mgs_blk<S = 1> (the next dot column prefetched into LDS during each
+    // all-gather): forced by GK_TUNE_RES_PF 1 for slabs up to 32 chunks of 512; by default
+    // (-1) where it measured faster than the strict kernels -- 16 chunks, the 4096^2 / 4 load:
+    // 2048^2 8.04 -> 7.64 us per projection; at 4 / 8 / 32 chunks it was slower or a tie
+    // (1024^2 3.78 -> 4.33, 1448^2 5.67 -> 5.77, 2896^2 15.0 -> 20.5; profiles/r05/
+    // ab_strict_pf_r05w.txt).  Not where the caller forced another variant.
+    const bool pf = !hh && tune_blk == 1 && var != gk::BLK_WONLY &&
+                    (tune_pf > 0 || (tune_pf < 0 && var == gk::BLK_R16 && tune_pc < 0 && tune_wonly <= 0));
+    if (!hh && (tune_blk > 1 || pf)) {
         // the blocked-projection MGS step (opt-in): the instantiation by the chunks of
         // 512 double2 a workgroup holds -- w in registers (+ LDS for the w-only build)
-        // and blocks of S columns cached where they fit (gk_blk.hpp)
+        // and blocks of S columns cached where they fit (gk_blk.hpp); S = 1
+        // (GK_TUNE_RES_PF): the strict step on the same kernel and its LDS prefetch
         p.G = gmax;
-        const int var = gk::blk_variant((n2 + (i64)gmax * 512 - 1) / ((i64)gmax * 512));
         const gk::BlkGeom g = gk::blk_geom(var, tune_blk);
         p.blk = tune_blk;
         p.bvar = var;
@@ -926,7 +937,7 @@ bool res_plan(gk_ctx *c, ResPlan &p, bool hh = false) {
     const int gmax = std::max(1, std::min(gk::RGMAX, c->res_cus / std::max(1, c->res_share)));
     const int cap = c->tune_res_r2 > 0 ? c->tune_res_r2 : RES_R2_BIG;
     plan_resident(c->nloc, gmax, cap, c->tune_res_lds, c->tune_res_wonly, hh,
-                  c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p, c->tune_res_pc, c->tune_res_blk);
+                  c->tune_nt > 0 || (c->tune_nt < 0 && c->nt_auto), p, c->tune_res_pc, c->tune_res_blk, c->tune_res_pf);
     if (p.wo && !hh && c->m + 1 > gk::WO_HMAX) return false;  // its H column: WO_HMAX entries of LDS
     return true;
 }
@@ -937,11 +948,11 @@ enum { RPI_VARIANT = 0, RPI_G, RPI_R2, RPI_L2, RPI_PF, RPI_CW, RPI_WO, RPI_NT, R
 void plan_info(const ResPlan &p, bool on, long long *info) {
     for (int k = 0; k < GK_RES_INFO_LEN; ++k) info[k] = 0;
     if (!on) return;
-    info[RPI_VARIANT] = p.blk > 1 ? GK_RES_BLOCKED
+    info[RPI_VARIANT] = p.bvar >= 0 ? GK_RES_BLOCKED
                         : p.pc    ? GK_RES_WCOL
                                   : (p.wo ? GK_RES_WONLY
                                           : (p.pf ? GK_RES_PREFETCH : (p.l2 > 0 ? GK_RES_PAIRS_LDS : GK_RES_PAIRS)));
-    info[RPI_BLK] = p.blk > 1 ? p.blk : 1;
+    info[RPI_BLK] = p.bvar >= 0 ? p.blk : 1;
     info[RPI_G] = p.G;
     info[RPI_R2] = p.r2;
     info[RPI_L2] = p.l2;
@@ -1035,7 +1046,7 @@ int launch_wpc_m(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
 }
 
 int launch_res(gk_ctx *c, const ResPlan &p, const gk::ResArgs &a) {
-    if (p.blk > 1) {
+    if (p.bvar >= 0) {
         if (a.mode != gk::RES_MGS) return set_err(GK_ERR_STATE, "the blocked step is the MGS-R step's only");
         const int e = gk::blk_launch(p.bvar, p.blk, a, p.G, p.lds, c->dev, c->st);
         if (e != 0)
@@ -1080,7 +1091,7 @@ int res_step(gk_ctx *c, int j, const ResPlan &p, const double *pin, int npin, do
         return set_err(GK_ERR_STATE, "resident flags %d need the w-only variant", flags);
     const bool pin_local = (flags & RESF_PIN_LOCAL) && mode != gk::RES_HH_DOWN && c->xs_on && c->nranks > 1;
     // exchanges of the launch
-    const int np = (mode == gk::RES_MGS ? (p.blk > 1 ? gk::blk_exchanges(j, p.blk) : 2 * j) : j) + (close ? 1 : 0);
+    const int np = (mode == gk::RES_MGS ? (p.bvar >= 0 ? gk::blk_exchanges(j, p.blk) : 2 * j) : j) + (close ? 1 : 0);
     if (c->res_tag > 0xF0000000u) {  // tags must never repeat within the granule region's lifetime
         HIPCHK(hipMemsetAsync(c->res_gath, 0, sizeof(gk::u64) * gk::RES_GATH_ALL, c->st));
         c->res_tag = 1;
@@ -2605,6 +2616,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
                 return set_err(GK_ERR_ARG, "GK_TUNE_RES_BLOCK %d: blocks of 1 (strict MGS-R), 2 or 4 projections", value);
             c->tune_res_blk = value;
             break;
+        case GK_TUNE_RES_PF: c->tune_res_pf = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_RES_LOOKAHEAD:  // (round 5: measured slower than the plain blocked step, removed)
             if (value != 0)
                 return set_err(GK_ERR_ARG, "GK_TUNE_RES_LOOKAHEAD was removed (look-ahead blocked step measured slower: "

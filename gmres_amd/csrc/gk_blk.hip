@@ -85,7 +85,7 @@ constexpr int BLK_WB_LDS = GK_BLK_WB_LDS;
 typedef __attribute__((address_space(3))) void lds_void_t;
 template <int RW, int LW, int RX, int LX, int S, int WBT, int TCH, int NT, int PFX = 0>
 __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
-    static_assert(S >= 2 && S <= RES_SMAX, "blocks of 2..RES_SMAX projections");
+    static_assert(S >= 1 && S <= RES_SMAX, "blocks of 1..RES_SMAX projections");
     static_assert(RX + LX <= RW, "the column cache covers register chunks of w only");
     static_assert(PFX <= RX && (PFX == 0 || (LW == 0 && LX == 0)), "the prefetch covers register-cached chunks");
     constexpr int NW = NT / 64, KM = 2 * S - 1;
@@ -106,7 +106,8 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     // in reverse -- its first block is the one the first sweep ended with (still on
     // chip), and the columns read last come back first (Infinity-Cache hits at the
     // split loads); in exact arithmetic the second sweep's h are all 0 in any order
-    auto blk_of = [&](int p) { return p < nb1 ? p : (BLK_REV2 ? 2 * nb1 - 1 - p : p - nb1); };
+    // (S = 1 is strict MGS-R: both sweeps in the reference's column order)
+    auto blk_of = [&](int p) { return p < nb1 ? p : (BLK_REV2 && S > 1 ? 2 * nb1 - 1 - p : p - nb1); };
     const i64 n2 = a.n >> 1, ld2 = a.ld >> 1;
     const i64 nch = a.nres2 / NT;
     const i64 c0 = (i64)blockIdx.x * a.r2e, cend = c0 + a.r2e < nch ? c0 + a.r2e : nch;
@@ -502,6 +503,19 @@ template <int S>
 struct BlkCfg;
 // (measured in the compile: the largest spill-free geometry of each variant; a
 // deeper batch or more cached register chunks spilled)
+#ifndef GK_BLK_S1_R32_RX
+#define GK_BLK_S1_R32_RX 8
+#endif
+// S = 1: the strict MGS-R step (h = <w, V_k> after the AXPY of V_{k-1}: gmres_mgsr.f90:341-360 in
+// its order) on this kernel's LDS prefetch of the next dot column during the all-gather
+// (GK_TUNE_RES_PF): the whole column for <= 16 chunks, RX of 32 otherwise (16 spilled)
+template <>
+struct BlkCfg<1> {
+    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4}, {8, 0, 8, 0, 512, 8}, {16, 0, 16, 0, 512, 16},
+                                            {32, 0, GK_BLK_S1_R32_RX, 0, 512, GK_BLK_S1_R32_RX},
+                                            {90, 38, 0, 0, 256, 0}};
+    static constexpr int wb[BLK_NVAR] = {4, 4, 4, 2, 4};
+};
 // (S = 2 at 16 chunks as a one-wave build -- the whole slab and both columns in registers, half
 // the next dot block prefetched -- was slower: 2048^2 8.04 -> 8.84 us per projection, its
 // all-gather wait 2.1 -> 3.2 us; profiles/r05/ab_blk_s2_onewave_r05v.txt)
@@ -561,7 +575,7 @@ int launch_s(int var, const ResArgs &a, int G, int lds, int dev, hipStream_t st)
 
 BlkGeom blk_geom(int var, int S) {
     if (var < 0 || var >= BLK_NVAR) return BlkGeom{0, 0, 0, 0, 0, 0};
-    return S == 4 ? BlkCfg<4>::g[var] : BlkCfg<2>::g[var];
+    return S == 4 ? BlkCfg<4>::g[var] : (S == 1 ? BlkCfg<1>::g[var] : BlkCfg<2>::g[var]);
 }
 
 int blk_variant(long long chunks512) {
@@ -570,6 +584,7 @@ int blk_variant(long long chunks512) {
 
 int blk_launch(int var, int S, const ResArgs &a, int G, int lds, int dev, hipStream_t st) {
     switch (S) {
+        case 1: return var == BLK_WONLY ? (int)hipErrorInvalidValue : launch_s<1>(var, a, G, lds, dev, st);
         case 2: return launch_s<2>(var, a, G, lds, dev, st);
         case 4: return launch_s<4>(var, a, G, lds, dev, st);
         default: return (int)hipErrorInvalidValue;

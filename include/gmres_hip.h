@@ -392,6 +392,13 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *   GK_TUNE_RES_LOOKAHEAD  removed in round 5 (a look-ahead build of the blocked step: parity
  *                          green, measured slower than the plain one -- DESIGN.md 3.1c); 1 is
  *                          refused
+ *   GK_TUNE_RES_PF         the STRICT MGS-R step on the blocked kernel with blocks of 1
+ *                          (k_mgs_blk<S = 1>: the reference's projection order, one all-gather
+ *                          per projection) whose next dot column is prefetched into LDS during
+ *                          each all-gather; gk_res_info reports variant blocked, blk 1.  -1
+ *                          (default): for slabs of 9..16 chunks of 512 double2 per workgroup
+ *                          (the 4096^2 / 4 load), where it measured faster; 1: for every slab
+ *                          up to 32 chunks; 0: never
  *   GK_TUNE_WATCHDOG_MS    limit of every host wait on the context's stream (gk_sync, the step
  *                          waits, gk_update_x ...); 0 (default) = twice the longest device
  *                          deadline plus a minute.  Past it the wait returns GK_ERR_COMM (a
@@ -434,6 +441,7 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_WATCHDOG_MS 24
 #define GK_TUNE_HH_NORM_ORDER 25
 #define GK_TUNE_RES_LOOKAHEAD 26
+#define GK_TUNE_RES_PF 27
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 /* Test hook: hold = 1 enqueues on the context's stream a wait for a mapped host
  * word that only hold = 0 writes (hipStreamWaitValue32) -- every later kernel of

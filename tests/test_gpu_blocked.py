@@ -214,3 +214,58 @@ def test_blocked_knob_rejects_other_sizes():
         with pytest.raises(Exception, match="removed"):  # the look-ahead build (round 5, measured slower)
             c.tune(nat.GK_TUNE_RES_LOOKAHEAD, 1)
 
+
+
+# ----------------------------------------------------- strict on the prefetch ---
+# GK_TUNE_RES_PF: the STRICT MGS-R step (blocks of 1: one all-gather per projection, the
+# reference's projection order) on k_mgs_blk's LDS prefetch of the next dot column.  Only
+# the in-thread dot summation order differs from the strict kernels: held to the strict
+# path's 1e-9 per cycle.
+
+
+@pytest.mark.parametrize("share,chunks", [(1, 4), (2, 8), (4, 16), (8, 32)])
+def test_strict_prefetch_build_vs_reference(share, chunks):
+    from gmres_amd import _native as nat
+    import gmres_amd as ga
+
+    g = REF["mgsr_omp_identity_1024_m95_12cyc_t8"]["hist_res"]
+    with ga.Context(1024, 95) as c:
+        c.set_rhs_ones()
+        c.tune(nat.GK_TUNE_RES_PF, 1)
+        if share > 1:
+            c.tune(nat.GK_TUNE_RES, 1)
+            c.tune(nat.GK_TUNE_RES_SHARE, share)
+        plan = c.res_info()
+        c.profile(True)
+        c.profile_reset()
+        r = ga.gmres_mgsr(c, 1e-15, max_cycles=12, want_verr=False, want_hist=True)
+        prof = c.profile_read()
+    assert plan["variant"] == "blocked" and plan["blk"] == 1 and plan["r2e"] == chunks, plan
+    assert prof["res"][1] >= 95 * 12 and prof["proj"][1] <= 1, prof
+    print(f"\n[strict S=1 share={share}] 1024^2 12 cycles: max rel dev vs reference {_dev(r.hist_res, g):.2e}")
+    assert np.allclose(r.hist_res, g, rtol=1e-9, atol=0)
+
+
+def test_strict_prefetch_build_ranks_and_ragged(oracle):
+    """Ragged slabs against the oracle (1e-9 over ten cycles) and 2 row-block ranks at
+    1448^2 (the 4096^2 / 8 load) against the reference's own cycle."""
+    from gmres_amd import _native as nat
+    import gmres_amd as ga
+
+    for N, m in ((127, 30), (100, 20), (96, 7)):
+        with ga.Context(N, m) as c:
+            c.set_rhs_ones()
+            c.tune(nat.GK_TUNE_RES_PF, 1)
+            assert c.res_info()["blk"] == 1 and c.res_info()["variant"] == "blocked"
+            r = ga.gmres_mgsr(c, 1e-15, max_cycles=10, want_verr=False, want_hist=True)
+        ref = oracle.gmres_mgsr(oracle.rhs_ones(N), N, m, variant=oracle.MGSR_OMP, max_cycles=10)
+        k = min(len(r.hist_res), len(ref.hist_res))
+        hi = [i for i in range(k) if ref.hist_res[i] > 1e-10]
+        assert np.allclose(np.asarray(r.hist_res)[hi], np.asarray(ref.hist_res)[hi], rtol=1e-9, atol=0), (N, m)
+    g = REF["mgsr_omp_identity_1448_m95_1cyc_t8"]["hist_res"]
+    with ga.Context(1448, 95) as c:
+        c.set_rhs_ones()
+        c.tune(nat.GK_TUNE_RES_PF, 1)
+        assert c.res_info()["r2e"] == 8
+        r = ga.gmres_mgsr(c, 1e-15, max_cycles=1, want_verr=False, want_hist=True)
+    assert r.hist_res[0] == pytest.approx(g[0], rel=1e-9)

@@ -2,11 +2,11 @@
 # Round 5, final tree: the whole GPU suite, smoke, the default bench line (with its config
 # legs and the reference CPU baseline) and its rocprofv3 kernel stats, the equal-load
 # strict points, and same-device rehearsals (2 ranks at 2896^2, 4 at 2048^2).
-OUT=gpurun_out/r05z
+OUT=gpurun_out/${TAG:-r05z}
 cd "$GRAFT_REPO_ROOT" || exit 1
 source tools/gpu_lib.sh
 export PYTHONUNBUFFERED=1
-T="python -u -m pytest -v --timeout 200 --timeout-method thread -p no:cacheprovider"
+T="python -u -m pytest -v -s --timeout 200 --timeout-method thread -p no:cacheprovider"
 B="python -u bench.py --no-cpu --no-configs"
 step gpu_tests 900 $T tests -m gpu
 tail -3 $OUT/gpu_tests.out
