@@ -134,7 +134,7 @@ struct gk_ctx {
     gk::u64 *res_gath = nullptr;                    // [RES_KMAX values][2][RGMAX][2] all-gather granules
     double *res_gm = nullptr;                       // blocked step: the cycle's Gram table [m+1][RES_SMAX]
     int tune_res_blk = 1;                           // blocked-projection MGS step: S (1 = strict MGS-R)
-    int tune_res_pf = -1;                           // strict MGS step on the blocked kernel's LDS prefetch (S = 1)
+    int tune_res_pf = 0;                            // strict MGS step on the blocked kernel's LDS prefetch (S = 1)
     int watchdog_ms = 0;                            // host watchdog of stream waits (0: from the device deadlines)
     bool broken = false;                            // the watchdog fired: a kernel of this context never completed
     unsigned *hold_word = nullptr, *hold_word_dev = nullptr;  // gk_debug_hold_stream's mapped word
@@ -823,7 +823,7 @@ bool wonly_pays(i64 n2, int G) { return wonly_bytes(n2, G) < pairs_bytes(n2, G);
 //   else w and the running column in 2 x 12 registers, plus (GK_TUNE_RES_LDS)
 //   w of 18 more chunks per workgroup in LDS, the rest streamed.
 void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bool hh, bool nt, ResPlan &p,
-                   int tune_pc = -1, int tune_blk = 1, int tune_pf = -1) {
+                   int tune_pc = -1, int tune_blk = 1, int tune_pf = 0) {
     const i64 n2 = nloc / 2;
     const i64 dcw = gk::RT - 64;
     // small vectors: no more workgroups than two chunks each (a cheaper all-gather)
@@ -853,13 +853,13 @@ void plan_resident(i64 nloc, int gmax, int cap, int tune_lds, int tune_wonly, bo
     // slower on it: 11.3-11.5 vs 9.6 us, ab_wpc_touch_r04e).
     const int var = gk::blk_variant((n2 + (i64)gmax * 512 - 1) / ((i64)gmax * 512));
     // The strict step on k_mgs_blk<S = 1> (the next dot column prefetched into LDS during each
-    // all-gather): forced by GK_TUNE_RES_PF 1 for slabs up to 32 chunks of 512; by default
-    // (-1) where it measured faster than the strict kernels -- 16 chunks, the 4096^2 / 4 load:
-    // 2048^2 8.04 -> 7.64 us per projection; at 4 / 8 / 32 chunks it was slower or a tie
-    // (1024^2 3.78 -> 4.33, 1448^2 5.67 -> 5.77, 2896^2 15.0 -> 20.5; profiles/r05/
-    // ab_strict_pf_r05w.txt).  Not where the caller forced another variant.
-    const bool pf = !hh && tune_blk == 1 && var != gk::BLK_WONLY &&
-                    (tune_pf > 0 || (tune_pf < 0 && var == gk::BLK_R16 && tune_pc < 0 && tune_wonly <= 0));
+    // all-gather), opt-in (GK_TUNE_RES_PF 1) for slabs up to 32 chunks of 512.  Faster than the
+    // strict kernels only at 16 chunks on one GPU (2048^2 8.04 -> 7.64 us per projection;
+    // 1024^2 3.78 -> 4.33, 1448^2 5.67 -> 5.77, 2896^2 15.0 -> 20.5: profiles/r05/
+    // ab_strict_pf_r05w.txt), and at the load it helps -- the 4096^2 / 4 split -- the 4-rank
+    // same-device rehearsal ran slower on it (1,061 vs 1,110 it/s, its all-gather wait 3.9 ->
+    // 7.6 us: reh4_2048_pf_r05x.json vs reh4_2048_r05z.json), so it is not the default.
+    const bool pf = !hh && tune_blk == 1 && var != gk::BLK_WONLY && tune_pf > 0;
     if (!hh && (tune_blk > 1 || pf)) {
         // the blocked-projection MGS step (opt-in): the instantiation by the chunks of
         // 512 double2 a workgroup holds -- w in registers (+ LDS for the w-only build)
@@ -2616,7 +2616,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
                 return set_err(GK_ERR_ARG, "GK_TUNE_RES_BLOCK %d: blocks of 1 (strict MGS-R), 2 or 4 projections", value);
             c->tune_res_blk = value;
             break;
-        case GK_TUNE_RES_PF: c->tune_res_pf = value < 0 ? -1 : (value != 0); break;
+        case GK_TUNE_RES_PF: c->tune_res_pf = value != 0; break;
         case GK_TUNE_RES_LOOKAHEAD:  // (round 5: measured slower than the plain blocked step, removed)
             if (value != 0)
                 return set_err(GK_ERR_ARG, "GK_TUNE_RES_LOOKAHEAD was removed (look-ahead blocked step measured slower: "

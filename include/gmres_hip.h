@@ -395,10 +395,10 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *   GK_TUNE_RES_PF         the STRICT MGS-R step on the blocked kernel with blocks of 1
  *                          (k_mgs_blk<S = 1>: the reference's projection order, one all-gather
  *                          per projection) whose next dot column is prefetched into LDS during
- *                          each all-gather; gk_res_info reports variant blocked, blk 1.  -1
- *                          (default): for slabs of 9..16 chunks of 512 double2 per workgroup
- *                          (the 4096^2 / 4 load), where it measured faster; 1: for every slab
- *                          up to 32 chunks; 0: never
+ *                          each all-gather; gk_res_info reports variant blocked, blk 1.  0
+ *                          (default): the strict kernels; 1: for every slab up to 32 chunks of
+ *                          512 double2 per workgroup (faster on one GPU at 16 chunks only;
+ *                          DESIGN.md 3.1c)
  *   GK_TUNE_WATCHDOG_MS    limit of every host wait on the context's stream (gk_sync, the step
  *                          waits, gk_update_x ...); 0 (default) = twice the longest device
  *                          deadline plus a minute.  Past it the wait returns GK_ERR_COMM (a

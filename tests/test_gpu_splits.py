@@ -45,13 +45,6 @@ CASES = [
 PROD = {1448: (4096, 8), 2048: (4096, 4), 2896: (4096, 2), 4096: (4096, 1)}
 
 
-def _variant(N, method, variant):
-    """The MGS-R step of the 4096^2 / 4 load runs the strict step on k_mgs_blk<S = 1>
-    (GK_TUNE_RES_PF auto: the next dot column prefetched into LDS); the reflection
-    chains keep the column-cache kernel."""
-    return "blocked" if (N == 2048 and method == "mgsr") else variant
-
-
 def _prod_nt(N):
     """The column load policy the production split selects (non-temporal once
     its slab outgrows the Infinity Cache): forced on the test grid, whose
@@ -143,8 +136,7 @@ def test_split_variant_in_process(N, variant, prod, R, method):
             c.xchg_local()
             _tune_forced(c, nt, R)
         plans = [c.res_info(hh=(method == "hh")) for c in ctxs]
-        want = _variant(N, method, variant)
-        assert all(p["variant"] == want and p["G"] == 256 // R for p in plans), (prod, plans)
+        assert all(p["variant"] == variant and p["G"] == 256 // R for p in plans), (prod, plans)
         assert len({(p["r2e"], p["l2e"], p["nt"]) for p in plans}) == 1, plans
 
         def work(r):
@@ -198,7 +190,7 @@ def test_first_dot_fold(N, variant, method):
                 c.xchg_local()
                 _tune_forced(c, nt, R)
                 c.tune(nat.GK_TUNE_RES_FOLD, fold)
-            assert all(c.res_info(hh=(method == "hh"))["variant"] == _variant(N, method, variant) for c in ctxs)
+            assert all(c.res_info(hh=(method == "hh"))["variant"] == variant for c in ctxs)
 
             def work(r):
                 try:
@@ -291,7 +283,7 @@ def test_split_variant_processes_ipc(R, N, variant, prod, method):
     for r in range(R):
         assert got[r][0] == "ok", got[r]
     vals = [got[r][1] for r in range(R)]
-    assert all(v[0]["variant"] == _variant(N, method, variant) and v[0]["G"] == 256 // R for v in vals), \
+    assert all(v[0]["variant"] == variant and v[0]["G"] == 256 // R for v in vals), \
         (prod, [v[0] for v in vals])
     _check_profile([v[1] for v in vals], method)
     assert all(np.array_equal(vals[0][2], v[2]) and np.array_equal(vals[0][3], v[3]) for v in vals)
