@@ -345,15 +345,22 @@ def maybe_self_launch(args, argv: list[str]) -> None:
     if vis < args.gpus and os.environ.get("GK_BENCH_SAME_DEVICE") != "1":
         print(f"bench.py: --gpus {args.gpus} but only {vis} GPU(s) visible", file=sys.stderr)
         sys.exit(2)
-    env = dict(os.environ, **plan["env"])
-    if os.environ.get("GK_BENCH_SAME_DEVICE") == "1" and "GPU_MAX_HW_QUEUES" not in os.environ:
-        # the N-rank rehearsal on ONE device: one hardware queue per rank process, so
-        # the N processes' queues do not oversubscribe the device's scheduler (8 x the
-        # default 4 hung the 8-process rehearsal in round 4; 8 x 1 runs, with the
-        # resident steps too: profiles/r05/reh8_same_device_r05_note.txt)
-        env["GPU_MAX_HW_QUEUES"] = "1"
-    p = subprocess.run(plan["cmd"], env=env)
+    p = subprocess.run(plan["cmd"], env=rank_env(os.environ, plan["env"]))
     sys.exit(p.returncode)
+
+
+def rank_env(environ, plan_env: dict) -> dict:
+    """The rank processes' environment.  The N-rank rehearsal on ONE device
+    (GK_BENCH_SAME_DEVICE=1) gets one hardware queue per rank process, so the N
+    processes' queues do not oversubscribe the device's scheduler (8 x the default
+    4 hung the 8-process rehearsal in round 4 and ran its warmup 50x slow in r05y;
+    8 x 1 runs, resident steps too: profiles/r05/reh8_same_device_r05_note.txt).
+    It overrides an inherited GPU_MAX_HW_QUEUES (the GPU box exports 4);
+    GK_BENCH_SAME_DEVICE_QUEUES picks another count."""
+    env = dict(environ, **plan_env)
+    if environ.get("GK_BENCH_SAME_DEVICE") == "1":
+        env["GPU_MAX_HW_QUEUES"] = environ.get("GK_BENCH_SAME_DEVICE_QUEUES", "1")
+    return env
 
 
 # ------------------------------------------------------------- device exchange

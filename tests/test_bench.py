@@ -190,6 +190,18 @@ def test_launcher_never_touches_hip():
     assert bench.visible_gpus() == 0 or os.path.exists("/dev/kfd")
 
 
+def test_same_device_rehearsal_gets_one_queue_per_rank():
+    """The same-device rehearsal overrides an inherited GPU_MAX_HW_QUEUES (the GPU
+    box exports 4: 8 ranks x 4 queues time-sliced the r05y 8-rank run); a real
+    multi-GPU run keeps the inherited value."""
+    box = {"GPU_MAX_HW_QUEUES": "4", "PATH": "/usr/bin"}
+    assert bench.rank_env(box, {"X": "1"}) == dict(box, X="1")
+    e = bench.rank_env(dict(box, GK_BENCH_SAME_DEVICE="1"), {})
+    assert e["GPU_MAX_HW_QUEUES"] == "1"
+    e = bench.rank_env(dict(box, GK_BENCH_SAME_DEVICE="1", GK_BENCH_SAME_DEVICE_QUEUES="2"), {})
+    assert e["GPU_MAX_HW_QUEUES"] == "2"
+
+
 def test_visible_gpus_respects_visibility_env(monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
     assert bench.visible_gpus() == 0
