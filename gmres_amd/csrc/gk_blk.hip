@@ -312,7 +312,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
             }
         }
         // streamed part: w and every column from HBM, one element pair at a time
-        for (i64 e = a.nres2 + (i64)blockIdx.x * NT + t; e < n2; e += sstride) {
+        for (i64 e = a.nres2 + (i64)res_stream_wg() * NT + t; e < n2; e += sstride) {
             double2 x = W2[e], bv[S];
 #pragma unroll
             for (int s = 0; s < S; ++s) {
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
             for (int d = 0; d < S; ++d) bv[d] = ldv<false>(D[d] + e);
             red(x, bv);
         }
-        if ((a.n & 1) && blockIdx.x == 0 && t == 0) {  // odd-length tail element
+        if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && t == 0) {  // odd-length tail element
             const i64 e = a.n - 1;
             double x = a.w[e];
 #pragma unroll
@@ -472,8 +472,8 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     }
     for (int k = 0; k < LW; ++k)
         if (l0 + k < lend) O2[(l0 + k) * NT + t] = outv(lw[k * NT + t]);
-    for (i64 e = a.nres2 + (i64)blockIdx.x * NT + t; e < n2; e += sstride) O2[e] = outv(W2[e]);
-    if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
+    for (i64 e = a.nres2 + (i64)res_stream_wg() * NT + t; e < n2; e += sstride) O2[e] = outv(W2[e]);
+    if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     clk.finish(a.stamps, RES_MGS);
     if (blockIdx.x == 0) {
         __syncthreads();
@@ -503,6 +503,15 @@ template <int S>
 struct BlkCfg;
 // (measured in the compile: the largest spill-free geometry of each variant; a
 // deeper batch or more cached register chunks spilled)
+// The LDS prefetch of the next dot block is capped at GK_BLK_PFX_KB per workgroup: what the
+// all-gather's latency can cover -- the rest streams in the pass, where compute overlaps it
+#ifndef GK_BLK_PFX_KB
+#define GK_BLK_PFX_KB 128
+#endif
+constexpr int pfx_cap(int chunks, int S, int nt) {
+    const int c = GK_BLK_PFX_KB * 1024 / (S * nt * 16);
+    return chunks < c ? chunks : c;
+}
 #ifndef GK_BLK_S1_R32_RX
 #define GK_BLK_S1_R32_RX 8
 #endif
@@ -511,8 +520,10 @@ struct BlkCfg;
 // (GK_TUNE_RES_PF): the whole column for <= 16 chunks, RX of 32 otherwise (16 spilled)
 template <>
 struct BlkCfg<1> {
-    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4}, {8, 0, 8, 0, 512, 8}, {16, 0, 16, 0, 512, 16},
-                                            {32, 0, GK_BLK_S1_R32_RX, 0, 512, GK_BLK_S1_R32_RX},
+    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, pfx_cap(4, 1, 512)},
+                                            {8, 0, 8, 0, 512, pfx_cap(8, 1, 512)},
+                                            {16, 0, 16, 0, 512, pfx_cap(16, 1, 512)},
+                                            {32, 0, GK_BLK_S1_R32_RX, 0, 512, pfx_cap(GK_BLK_S1_R32_RX, 1, 512)},
                                             {90, 38, 0, 0, 256, 0}};
     static constexpr int wb[BLK_NVAR] = {4, 4, 4, 2, 4};
 };
@@ -521,7 +532,8 @@ struct BlkCfg<1> {
 // all-gather wait 2.1 -> 3.2 us; profiles/r05/ab_blk_s2_onewave_r05v.txt)
 template <>
 struct BlkCfg<2> {
-    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4}, {8, 0, 8, 0, 512, 8}, {16, 0, 7, 9, 512, 0},
+    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, pfx_cap(4, 2, 512)},
+                                            {8, 0, 8, 0, 512, pfx_cap(8, 2, 512)}, {16, 0, 7, 9, 512, 0},
                                             {32, 0, 1, 9, 512, 0}, {90, 38, 0, 0, 256, 0}};
     static constexpr int wb[BLK_NVAR] = {4, 4, 4, 2, 4};
 };
@@ -535,8 +547,8 @@ struct BlkCfg<2> {
 // profiles/r05/ab_blk_s4_onewave_r05t.txt)
 template <>
 struct BlkCfg<4> {
-    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, 4},
-                                            GK_BLK_S4_R8_1W ? BlkGeom{16, 0, 16, 0, 256, 8} : BlkGeom{8, 0, 8, 0, 512, 0},
+    static constexpr BlkGeom g[BLK_NVAR] = {{4, 0, 4, 0, 512, pfx_cap(4, 4, 512)},
+                                            GK_BLK_S4_R8_1W ? BlkGeom{16, 0, 16, 0, 256, pfx_cap(8, 4, 256)} : BlkGeom{8, 0, 8, 0, 512, 0},
                                             {16, 0, 2, 4, 512, 0}, {32, 0, 0, 4, 512, 0}, {88, 38, 0, 0, 256, 0}};
     static constexpr int wb[BLK_NVAR] = {4, GK_BLK_S4_R8_1W ? 4 : 2, 2, 1, 2};
 };

@@ -843,7 +843,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
             if (data && l0 + k < lend) lw[k * DT + td] = W2[(l0 + k) * DT + td];
     }
     const i64 sstride = (i64)gridDim.x * DT;
-    const i64 sbase = a.nres2 + (i64)blockIdx.x * DT + td;
+    const i64 sbase = a.nres2 + (i64)res_stream_wg() * DT + td;
     ResClock clk;
     clk.start(a.stamps);
     int xi = 0;  // exchange index
@@ -874,7 +874,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                 acc = acc + wv.x * bv.x;
                 acc = acc + wv.y * bv.y;
             }
-            if ((a.n & 1) && blockIdx.x == 0 && td == 0) acc = acc + a.w[a.n - 1] * a.V[(i64)q * a.ld + a.n - 1];
+            if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && td == 0) acc = acc + a.w[a.n - 1] * a.V[(i64)q * a.ld + a.n - 1];
         }
         acc = wave_sum(acc);
         if ((t & 63) == 0) sm[t >> 6] = acc;
@@ -989,7 +989,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
                     }
                 }
             }
-            if ((a.n & 1) && blockIdx.x == 0 && td == 0) {  // odd-length tail element
+            if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && td == 0) {  // odd-length tail element
                 const i64 e = a.n - 1;
                 const double x = a.w[e] - ch * a.V[(i64)i * a.ld + e];
                 a.w[e] = x;
@@ -1059,7 +1059,7 @@ __global__ __launch_bounds__(RT, 2) void k_mgs_res(ResArgs a) {
             const double2 v = W2[e];
             O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
         }
-        if ((a.n & 1) && blockIdx.x == 0 && td == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
+        if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && td == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     }
     clk.finish(a.stamps, mode);
     if (blockIdx.x == 0) {  // H(1:j+1, j) to the device column and the mapped host mirror
@@ -1177,7 +1177,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
     clk.start(a.stamps);
     int touch_sink = 0;
     const i64 sstride = (i64)gridDim.x * WT;
-    const i64 sbase = a.nres2 + (i64)blockIdx.x * WT + t;
+    const i64 sbase = a.nres2 + (i64)res_stream_wg() * WT + t;
     double2 wr[RW];
     if (mode == RES_HH_DOWN && a.unit_init) {
         // w = e_u built in place (gmres_hh.f90:257-264): no k_set_unit launch, no read
@@ -1189,7 +1189,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         for (int k = 0; k < LW; ++k)
             if (l0 + k < lend) lw[k * WT + t] = unit2((l0 + k) * WT + t);
         for (i64 e = sbase; e < n2; e += sstride) W2[e] = unit2(e);
-        if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.w[a.n - 1] = (a.n - 1 == u) ? 1.0 : 0.0;
+        if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && t == 0) a.w[a.n - 1] = (a.n - 1 == u) ? 1.0 : 0.0;
     } else {
 #pragma unroll
         for (int k = 0; k < RW; ++k) wr[k] = (c0 + k < cend) ? W2[(c0 + k) * WT + t] : double2{0.0, 0.0};
@@ -1281,7 +1281,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
                 }
             }
         }
-        if ((a.n & 1) && blockIdx.x == 0 && t == 0) {  // odd-length tail element
+        if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && t == 0) {  // odd-length tail element
             const i64 e = a.n - 1;
             const double x = a.w[e] - ch * a.V[(i64)i * a.ld + e];
             a.w[e] = x;
@@ -1383,7 +1383,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             }
         if (up) {
             for (i64 e = sbase; e < n2; e += sstride) sq_acc(acc, W2[e], e, tail0, 2 * e < tail0 + 2);
-            if ((a.n & 1) && blockIdx.x == 0 && t == 0 && a.n - 1 >= tail0) {
+            if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && t == 0 && a.n - 1 >= tail0) {
                 const double x = a.w[a.n - 1];
                 acc = acc + x * x;
             }
@@ -1439,7 +1439,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
             fix_sq(acc2, v, e, chk);
             if (chk) W2[e] = v;
         }
-        if ((a.n & 1) && blockIdx.x == 0 && t == 0) {
+        if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && t == 0) {
             double x = a.w[a.n - 1];
             if (a.n - 1 <= f) {
                 fix1(x, a.n - 1);
@@ -1465,7 +1465,7 @@ __global__ __launch_bounds__(WT, 1) void k_mgs_wres(ResArgs a) {
         const double2 v = W2[e];
         O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
     }
-    if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
+    if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     clk.finish(a.stamps, mode);
     if (mode == RES_MGS && blockIdx.x == 0) {
         __syncthreads();
@@ -1518,7 +1518,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_wpc(ResArgs a) {
     ResClock clk;
     clk.start(a.stamps);
     const i64 sstride = (i64)gridDim.x * NT;
-    const i64 sbase = a.nres2 + (i64)blockIdx.x * NT + t;
+    const i64 sbase = a.nres2 + (i64)res_stream_wg() * NT + t;
     double2 wr[RW], xc[RX > 0 ? RX : 1];
     {  // w, and the AXPY column of pass 0 into the cache
         const double2 *__restrict__ C2 = V2 + (i64)res_col(mode, j, 0) * ld2;
@@ -1604,7 +1604,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_wpc(ResArgs a) {
                 }
             }
         }
-        if ((a.n & 1) && blockIdx.x == 0 && t == 0) {  // odd-length tail element
+        if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && t == 0) {  // odd-length tail element
             const i64 e = a.n - 1;
             const double x = a.w[e] - ch * a.V[(i64)i * a.ld + e];
             a.w[e] = x;
@@ -1700,7 +1700,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_wpc(ResArgs a) {
         const double2 v = W2[e];
         O2[e] = hn != 0.0 ? double2{v.x / hn, v.y / hn} : double2{0.0, 0.0};
     }
-    if ((a.n & 1) && blockIdx.x == 0 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
+    if ((a.n & 1) && blockIdx.x == gridDim.x - 1 && t == 0) a.vout[a.n - 1] = hn != 0.0 ? a.w[a.n - 1] / hn : 0.0;
     clk.finish(a.stamps, mode);
     if (blockIdx.x == 0) {
         __syncthreads();

@@ -182,7 +182,11 @@ def test_1024_twelve_cycle_history_vs_reference(method, prec, key):
 #      2/4/8 OpenMP threads (64^2 m=20 2 cycles, 128^2 m=30 3 cycles and to
 #      convergence):
 #        MGS-R v_err(2:n_out+1): last (cumulative) entry within 0.24 decades,
-#              entrywise median <= 0.27, entrywise max 0.54 decades;
+#              entrywise median <= 0.27, entrywise max 0.54 decades; over every
+#              pair of 1..8 threads, two runs (tools/verr_spread.py,
+#              profiles/r05/verr_oracle_spread_r05.txt; the threaded oracle is
+#              not run-to-run deterministic): last 0.31, median 0.36, entrywise
+#              max 1.25 decades -- the first entries, a few rounding errors each;
 #        HH calculate_verr(2:n_out): sum within 0.36 decades, entrywise median
 #              <= 0.65, entrywise max 2.8 decades (single terms are pure noise).
 #      Tolerances: about twice the measured spread, in decades.
@@ -192,8 +196,8 @@ def _decades(a, b):
 
 def _mgs_verr_close(a, b):
     d = _decades(a, b)
-    assert d[-1] <= 0.5, (a[-1], b[-1])
-    assert np.median(d) <= 0.5 and d.max() <= 1.0, d
+    assert d[-1] <= 0.6, (a[-1], b[-1])
+    assert np.median(d) <= 0.7 and d.max() <= 2.5, d
 
 
 def _hh_verr_close(a, b, below=0.7, above=0.7):

@@ -12,7 +12,7 @@ Prints one JSON line per traced step: means / percentiles of skew and
 propagation, the share of exchanges each XCD (blockIdx % 8) was last in, and
 the spread of publish times per exchange.
 
-  python tools/res_trace.py [--grid 4096] [--m 95] [--steps 16,48,80]
+  python tools/res_trace.py [--grid 4096] [--m 95] [--steps 16,48,80] [--tune 23=4]
 """
 import argparse
 import json
@@ -75,11 +75,15 @@ def main() -> None:
     ap.add_argument("--grid", type=int, default=4096)
     ap.add_argument("--m", type=int, default=95)
     ap.add_argument("--steps", default="16,48,80")
+    ap.add_argument("--tune", action="append", default=[], help="K=V: a GK_TUNE_* knob (e.g. 23=4, the blocked step)")
     a = ap.parse_args()
     import gmres_amd as ga
 
     with ga.Context(a.grid, a.m) as c:
         c.set_rhs_ones()
+        for kv in a.tune:
+            k, v = kv.split("=")
+            c.tune(int(k), int(v))
 
         def run():
             return ga.gmres_mgsr(c, 1e-15, max_cycles=1, want_verr=False)
