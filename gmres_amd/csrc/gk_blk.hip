@@ -503,10 +503,13 @@ template <int S>
 struct BlkCfg;
 // (measured in the compile: the largest spill-free geometry of each variant; a
 // deeper batch or more cached register chunks spilled)
-// The LDS prefetch of the next dot block is capped at GK_BLK_PFX_KB per workgroup: what the
-// all-gather's latency can cover -- the rest streams in the pass, where compute overlaps it
+// The LDS prefetch of the next dot block is capped at GK_BLK_PFX_KB per workgroup: about what
+// HBM delivers to one CU during an all-gather -- the rest streams in the pass, where compute
+// overlaps it, instead of holding the pass back at the wait for the prefetch (96 vs 128 / 80:
+// 1024^2 S = 4 2.44 -> 2.30 us per projection, 1448^2 S = 2 4.25 -> 4.07, S = 4 3.95 -> 3.90;
+// profiles/r05/ab_blk_pfx_kb_r05ae.txt)
 #ifndef GK_BLK_PFX_KB
-#define GK_BLK_PFX_KB 128
+#define GK_BLK_PFX_KB 96
 #endif
 constexpr int pfx_cap(int chunks, int S, int nt) {
     const int c = GK_BLK_PFX_KB * 1024 / (S * nt * 16);

@@ -95,7 +95,10 @@ def test_blocked_plan_of_every_split(N, R, S, want):
     assert p["variant"] == "blocked" and p["blk"] == S and p["G"] == 256, p
     assert (p["wt"], p["r2e"], p["l2e"], p["r2"], p["l2"]) == want, p
     lw = 38 if p["wt"] == 256 and p["r2e"] > 32 else 0  # (the w-only build; not the one-wave S = 4 one)
-    pfx = {(512, 4): 4, (512, 8): 8, (256, 16): 8}.get((p["wt"], p["r2e"]), 0)  # LDS prefetch of small slabs
+    # LDS prefetch of small slabs: the next dot block's first chunks, capped at 96 KiB per
+    # workgroup (GK_BLK_PFX_KB; profiles/r05/ab_blk_pfx_kb_r05ae.txt)
+    chunks = {(512, 4): 4, (512, 8): 8, (256, 16): 8}.get((p["wt"], p["r2e"]), 0)
+    pfx = min(chunks, 96 * 1024 // (S * p["wt"] * 16))
     assert p["lds"] == (lw + S * (p["l2"] + pfx)) * p["wt"] * 16 and p["lds"] + 5 * 1024 <= 160 * 1024, p
     # the whole slab is resident except the w-only S = 4 build's two streamed chunks
     assert p["nres2"] <= N * nl // 2
