@@ -602,6 +602,51 @@ def diagnostics(ctx, args, run, ctl, world: int) -> dict:
                     "all-gather (tools/res_split.py); collective = one partial-slab all-reduce / one halo exchange"}
 
 
+def blocked_leg_block(grid: int, world: int) -> int:
+    """The projection block of the N-rank blocked leg: per GPU load, the S that measured
+    fastest on one GPU at that load (tools/predict_scaling.py POINTS_BLOCKED):
+    4 at the 4096^2 / 8 load (1448^2) and below, 2 above."""
+    return 4 if grid * grid // world <= 1448 * 1448 * 11 // 10 else 2
+
+
+def blocked_leg(ctx, args, run, ctl, world: int, cycles: int = 2) -> dict:
+    """After the timed region, N > 1 only (not `value`, which stays the reference's strict
+    MGS-R): the same N-rank workload on the opt-in blocked-projection step
+    (GK_TUNE_RES_BLOCK, one in-launch all-gather -- and one cross-GPU rank hop -- per
+    block of S projections), so a multi-GPU run measures what DESIGN.md 6.1 predicts for
+    it: a 1-cycle solve from x0 = 0 checked against the reference's history, then
+    `cycles` timed cycles, max over ranks, and the in-launch split."""
+    S = blocked_leg_block(args.grid, world)
+    ok, why, out = 1, "", {}
+    try:
+        ctx.tune(23, S)  # GK_TUNE_RES_BLOCK (re-plans, drops captured graphs)
+        ctx.zero_x()
+        chk = run(1, hist=True)
+        ctx.sync()
+        ctl.barrier()
+        t0 = time.perf_counter()
+        r = run(cycles, want_x=False)
+        ctx.sync()
+        el = time.perf_counter() - t0
+        out = {"res": r, "chk": chk, "el": el, "plan": ctx.res_info()}
+    except Exception as e:  # noqa: BLE001 - every rank reports, then all agree below
+        ok, why = 0, str(e)
+    if ctl.allreduce(ok, "min") != 1:
+        return {"projection_block": S, "error": why[:300] or "a peer rank failed the blocked leg"}
+    el = ctl.allreduce(out["el"], "max")
+    split = diagnostics(ctx, args, run, ctl, world).get("resident_split_per_unit_us")
+    ctx.tune(23, 1)
+    r = out["res"]
+    iters = (r.n_cycles - 1) * args.m + r.n_out
+    check = history_vs_golden(out["chk"].hist_res, *GOLDEN_OF.get((args.grid, args.m, args.prec, args.method),
+                                                                   (None, None)))
+    return {"projection_block": S, "it_s": round(iters / el, 3), "ms_per_cycle": round(el / max(r.n_cycles, 1) * 1e3, 3),
+            "cycles": r.n_cycles, "resident_variant": out["plan"].get("variant"),
+            "resident_split_per_unit_us": split, "check": check,
+            "note": "opt-in blocked-projection MGS-R step (GK_TUNE_RES_BLOCK) on the same ranks after the timed "
+                    "region; value is the strict step"}
+
+
 # ------------------------------------------------------- BASELINE configs ---
 GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
 # cycle-1 true residual of each workload from x0 = 0: the reference's own run
@@ -887,6 +932,10 @@ def main() -> None:
     log("diagnostics done")
     if diag is not None:
         diag["pcie_inclusive"] = pcie_inclusive(ctx, args, run, ctl, line0, nlines)
+        if (world > 1 and args.method == "mgsr" and fallback is None
+                and not any(kv.split("=")[0] == "23" for kv in args.tune)):
+            log("blocked leg")
+            diag["blocked_leg"] = blocked_leg(ctx, args, run, ctl, world)
 
     cheb_sten = plan.get("cheb_sten", 0) == 1
     roof = roofline_entry(prof, args, ctx.nloc, cycles, world, plan) if rank == 0 else None

@@ -202,6 +202,16 @@ def test_same_device_rehearsal_gets_one_queue_per_rank():
     assert e["GPU_MAX_HW_QUEUES"] == "2"
 
 
+def test_blocked_leg_block_follows_the_per_gpu_load():
+    """The N-rank blocked leg takes S = 4 at the 4096^2 / 8 load (1448^2) and S = 2 above
+    (tools/predict_scaling.py POINTS_BLOCKED)."""
+    assert bench.blocked_leg_block(4096, 8) == 4
+    assert bench.blocked_leg_block(4096, 4) == 2
+    assert bench.blocked_leg_block(4096, 2) == 2
+    assert bench.blocked_leg_block(8192, 8) == 2
+    assert bench.blocked_leg_block(1448, 2) == 4
+
+
 def test_visible_gpus_respects_visibility_env(monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
     assert bench.visible_gpus() == 0
