@@ -364,3 +364,9 @@ def test_read_scale_finds_bench_lines_in_a_driver_file():
                         "predicted_wait_per_projection_us": [4.0, 7.0]}]}
     (row,) = read_scale.compare(lines, pred)
     assert row["verdict"] == "inside band" and row["wait_us"] == 5.0 and row["variant"] == "w+column"
+    # round 5's two tables, and the N-rank line's blocked leg against the blocked one
+    line["diagnostics"]["blocked_leg"] = {"it_s": 470.0, "projection_block": 2}
+    pred5 = {"strict": pred, "blocked": {"points": [{"world": 2, "grid": 4096, "predicted_it_s": [480.0, 520.0]}]}}
+    doc = {"runs": [{"n": 2, "run": {"stdout_tail": json.dumps(line)}}]}
+    (row,) = read_scale.compare(read_scale.bench_lines(doc), pred5)
+    assert row["verdict"] == "inside band" and row["blocked_S"] == 2 and row["blocked_verdict"] == "below band"
