@@ -43,11 +43,11 @@ M = 95
 # per-GPU load of each point -> the single-GPU bench line measured at that load
 POINTS = [
     # (label, world, global grid, equal-load single-GPU grid, bench JSON under profiles/)
-    ("4096^2 on 1 GPU", 1, 4096, 4096, "r05/bench_point_4096_strict_r05l.json"),
-    ("4096^2 on 2 GPUs", 2, 4096, 2896, "r05/bench_point_2896_strict_r05b.json"),
-    ("4096^2 on 4 GPUs", 4, 4096, 2048, "r05/bench_point_2048_strict_r05b.json"),
-    ("4096^2 on 8 GPUs", 8, 4096, 1448, "r05/bench_point_1448_strict_r05b.json"),
-    ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r05/bench_point_2896_strict_r05b.json"),
+    ("4096^2 on 1 GPU", 1, 4096, 4096, "r05/bench_point_4096_strict_r05z2.json"),
+    ("4096^2 on 2 GPUs", 2, 4096, 2896, "r05/bench_point_2896_strict_r05z2.json"),
+    ("4096^2 on 4 GPUs", 4, 4096, 2048, "r05/bench_point_2048_strict_r05z2.json"),
+    ("4096^2 on 8 GPUs", 8, 4096, 1448, "r05/bench_point_1448_strict_r05z2.json"),
+    ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r05/bench_point_2896_strict_r05z2.json"),
 ]
 # the same points with the opt-in blocked-projection step (GK_TUNE_RES_BLOCK S, round 5):
 # per point the block size that measured fastest at that load, one in-launch all-gather
