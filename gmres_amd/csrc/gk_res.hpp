@@ -195,11 +195,8 @@ enum { RK_NONE = 0, RK_DOT = 1, RK_NORM = 2 };  // reduction closing a pass
 // down: when the resident chunks do not fill the grid (1448^2, 2896^2: a ragged last chunk)
 // the last workgroup's chunk range is the short one, so the ragged tail rides there instead
 // of lengthening workgroup 0's pass -- which the all-gather trace showed as the straggler of
-// every exchange (profiles/r05/res_trace_1448_r05ac.txt)
-#ifndef GK_RES_STREAM_WG0  // (A/B only: 1 = the round-4 assignment from workgroup 0 up)
-#define GK_RES_STREAM_WG0 0
-#endif
-__device__ __forceinline__ unsigned res_stream_wg() { return GK_RES_STREAM_WG0 ? blockIdx.x : gridDim.x - 1 - blockIdx.x; }
+// every exchange (profiles/r05/res_trace_1448_r05ac.txt; A/B ab_stream_wg_r05ad.txt, _4096_r05ag.txt)
+__device__ __forceinline__ unsigned res_stream_wg() { return gridDim.x - 1 - blockIdx.x; }
 
 __device__ __forceinline__ int res_np(int mode, int j) { return mode == RES_MGS ? 2 * j : j; }
 __device__ __forceinline__ int res_col(int mode, int j, int p) {
