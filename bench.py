@@ -74,8 +74,9 @@ def res_regions(plan: dict, nloc: int) -> dict:
     (pairs); w+column: the plan's "wt" (512 since round 4's two-wave build)."""
     n2 = nloc // 2
     var = plan["variant"]
-    if var == "blocked":  # k_mgs_blk: the w-only build (256 threads) or a block-cache build
-        var = "w-only" if int(plan["wt"]) == 256 else "w+column"
+    if var == "blocked":  # k_mgs_blk: the w-only build (no block cache) or a block-cache build
+        # (the one-wave S = 4 build also runs 256 threads, with its whole block cached)
+        var = "w-only" if int(plan["r2"]) + int(plan["l2"]) == 0 else "w+column"
     dt = 256 if var in ("w-only", "w+column") else (448 if plan.get("cw") else 512)
     if var in ("w-only", "w+column") and plan.get("wt"):
         dt = int(plan["wt"])  # threads per workgroup = double2 per chunk
@@ -491,7 +492,8 @@ def roofline_entry(prof: dict, args, nloc: int, cycles: int, world: int, plan: d
         roof["ceiling"] = "hbm: every compulsory byte is a DRAM byte (non-temporal column loads / register reuse)"
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf) and on_res and args.method == "mgsr":
-        key, scale = pmc_lookup(json.load(open(tf)), variant, nloc, m, args.prec, args.method,
+        pvar = f"blocked{(plan or {}).get('blk')}" if variant == "blocked" else variant  # bytes depend on S
+        key, scale = pmc_lookup(json.load(open(tf)), pvar, nloc, m, args.prec, args.method,
                                 int((plan or {}).get("G", 256)))
         pm = json.load(open(tf)).get(key) if key else None
         if pm and "per_step" in pm:

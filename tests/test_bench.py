@@ -120,6 +120,21 @@ def test_resident_byte_model_follows_the_variant():
     assert per_pass == pytest.approx(8.0, rel=2e-3)
 
 
+def test_blocked_byte_model_of_the_one_wave_build():
+    """The one-wave S = 4 blocked build (256 threads like the w-only one, but its whole block
+    cached): 8 B per unknown per pass, as its PMC traffic over a full cycle at 1448^2 shows
+    (profiles/r05/pmc_*_bench_1448_blk4_cycle_r05am.csv: 8.06 B, traffic / model 0.99-1.004)."""
+    import gmres_amd as ga
+
+    n = 4096 * 512
+    p = ga.res_plan_query(n, 256, 1, False, -1, block=4)
+    assert (p["variant"], p["wt"], p["r2"]) == ("blocked", 256, 16)
+    per_pass = (bench.res_launch_bytes(p, n, 97) - bench.res_launch_bytes(p, n, 96)) / n
+    assert per_pass == pytest.approx(8.0)
+    p = ga.res_plan_query(4096 * 4096, 256, 1, False, -1, block=4)  # the w-only blocked build
+    assert bench.res_regions(p, 4096 * 4096)["pairs"] == 0
+
+
 def test_roofline_entry_is_a_fraction():
     """The round-1 bench's sampled launches (4,100 us per step launch at j = 16..80
     over 20 cycles) give frac ~0.8 on the fused-minimum model, and the

@@ -56,7 +56,7 @@ def res_fit(a):
     import gmres_amd as ga
 
     nl = max(k for _, k in ga.slab_partition(a.grid, a.gpus))
-    plan = ga.res_plan_query(a.grid * nl, 256, 1, a.method == "hh", -1)
+    plan = ga.res_plan_query(a.grid * nl, 256, 1, a.method == "hh", -1, block=a.block)
     if a.variant and plan["variant"] != a.variant:
         raise SystemExit(f"the plan query selects {plan['variant']}, not {a.variant}")
     model = {int(j): bench.res_launch_bytes(plan, n, 2 * int(j), mgs=True) for j in js}
@@ -71,7 +71,9 @@ def res_fit(a):
                        "of one full cycle, FETCH_SIZE x2 gfx950 correction; L2<->fabric bytes incl. "
                        "Infinity-Cache hits)"}
     db = json.load(open(a.out)) if os.path.exists(a.out) else {}
-    db[bench.pmc_key(plan["variant"], n, a.m, a.prec, a.method)] = entry
+    pvar = f"blocked{a.block}" if plan["variant"] == "blocked" else plan["variant"]  # (bench.roofline_entry)
+    entry["projection_block"] = a.block
+    db[bench.pmc_key(pvar, n, a.m, a.prec, a.method)] = entry
     json.dump(db, open(a.out, "w"), indent=1)
     print(json.dumps({k: v for k, v in entry.items() if k != "per_step"}, indent=1))
 
@@ -91,6 +93,7 @@ def main():
                          "fit bytes per launch = fixed + per_projection * 2j")
     ap.add_argument("--probe-m", type=int, default=95, help="resident launches of the traced cycle (= m)")
     ap.add_argument("--variant", default=None, help="the resident variant expected to have run (checked)")
+    ap.add_argument("--block", type=int, default=1, help="GK_TUNE_RES_BLOCK of the traced run (blocked step: 2 / 4)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
