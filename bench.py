@@ -611,17 +611,18 @@ def blocked_leg_block(grid: int, world: int) -> int:
     return 4 if grid * grid // world <= 1448 * 1448 * 11 // 10 else 2
 
 
-def blocked_leg(ctx, args, run, ctl, world: int, cycles: int = 2) -> dict:
+def blocked_leg(ctx, args, run, ctl, world: int, cycles: int = 2, key: int = 23, S: int | None = None) -> dict:
     """After the timed region, N > 1 only (not `value`, which stays the reference's strict
-    MGS-R): the same N-rank workload on the opt-in blocked-projection step
-    (GK_TUNE_RES_BLOCK, one in-launch all-gather -- and one cross-GPU rank hop -- per
-    block of S projections), so a multi-GPU run measures what DESIGN.md 6.1 predicts for
-    it: a 1-cycle solve from x0 = 0 checked against the reference's history, then
-    `cycles` timed cycles, max over ranks, and the in-launch split."""
-    S = blocked_leg_block(args.grid, world)
+    MGS-R on the default kernels): the same N-rank workload on an opt-in step -- by default
+    the blocked-projection step (GK_TUNE_RES_BLOCK, one in-launch all-gather -- and one
+    cross-GPU rank hop -- per block of S projections), or (key 27, GK_TUNE_RES_PF) the strict
+    step on the prefetching blocked kernel -- so a multi-GPU run measures what DESIGN.md 6.1
+    predicts for it: a 1-cycle solve from x0 = 0 checked against the reference's history,
+    then `cycles` timed cycles, max over ranks, and the in-launch split."""
+    S = blocked_leg_block(args.grid, world) if S is None else S
     ok, why, out = 1, "", {}
     try:
-        ctx.tune(23, S)  # GK_TUNE_RES_BLOCK (re-plans, drops captured graphs)
+        ctx.tune(key, S)  # GK_TUNE_RES_BLOCK / GK_TUNE_RES_PF (re-plans, drops captured graphs)
         ctx.zero_x()
         chk = run(1, hist=True)
         ctx.sync()
@@ -637,16 +638,18 @@ def blocked_leg(ctx, args, run, ctl, world: int, cycles: int = 2) -> dict:
         return {"projection_block": S, "error": why[:300] or "a peer rank failed the blocked leg"}
     el = ctl.allreduce(out["el"], "max")
     split = diagnostics(ctx, args, run, ctl, world).get("resident_split_per_unit_us")
-    ctx.tune(23, 1)
+    ctx.tune(key, 1 if key == 23 else 0)
     r = out["res"]
     iters = (r.n_cycles - 1) * args.m + r.n_out
     check = history_vs_golden(out["chk"].hist_res, *GOLDEN_OF.get((args.grid, args.m, args.prec, args.method),
                                                                    (None, None)))
-    return {"projection_block": S, "it_s": round(iters / el, 3), "ms_per_cycle": round(el / max(r.n_cycles, 1) * 1e3, 3),
+    what = ("opt-in blocked-projection MGS-R step (GK_TUNE_RES_BLOCK)" if key == 23 else
+            "strict MGS-R on the prefetching blocked kernel, blocks of 1 (GK_TUNE_RES_PF)")
+    return {"projection_block": S if key == 23 else 1, "it_s": round(iters / el, 3),
+            "ms_per_cycle": round(el / max(r.n_cycles, 1) * 1e3, 3),
             "cycles": r.n_cycles, "resident_variant": out["plan"].get("variant"),
             "resident_split_per_unit_us": split, "check": check,
-            "note": "opt-in blocked-projection MGS-R step (GK_TUNE_RES_BLOCK) on the same ranks after the timed "
-                    "region; value is the strict step"}
+            "note": f"{what} on the same ranks after the timed region; value is the strict step on the default kernels"}
 
 
 # ------------------------------------------------------- BASELINE configs ---
@@ -938,6 +941,8 @@ def main() -> None:
                 and not any(kv.split("=")[0] == "23" for kv in args.tune)):
             log("blocked leg")
             diag["blocked_leg"] = blocked_leg(ctx, args, run, ctl, world)
+            log("strict prefetch leg")
+            diag["strict_prefetch_leg"] = blocked_leg(ctx, args, run, ctl, world, key=27, S=1)
 
     cheb_sten = plan.get("cheb_sten", 0) == 1
     roof = roofline_entry(prof, args, ctx.nloc, cycles, world, plan) if rank == 0 else None

@@ -41,6 +41,15 @@ constexpr bool BLK_REV2 = GK_BLK_REV2 != 0;  // the second sweep's blocks in rev
 // on); 0: the default policy, so a column read again within the Infinity Cache's
 // reach (the reversed second sweep, the next step's first sweep) is a hit (A/B knob)
 constexpr bool BLK_DOT_NT = GK_BLK_DOT_NT != 0;
+#ifndef GK_BLK_PF_SPLIT
+#define GK_BLK_PF_SPLIT 1
+#endif
+// the strict step on this kernel (S = 1, GK_TUNE_RES_PF): the prefetch during an all-gather
+// from the waves that do not poll it, so the poll -- and on N ranks a rank-total pusher's push --
+// does not queue behind it (4-rank rehearsal 935 -> 968 it/s, single GPU +1 %:
+// profiles/r05/ab_strict_pf_split_r05aq.txt); blocks of 2 / 4 keep every wave its own
+// elements (a wash there: ab_blk_pf_split_r05ak.txt)
+constexpr bool BLK_PF_SPLIT = GK_BLK_PF_SPLIT != 0;
 #ifndef GK_BLK_WB_LDS
 #define GK_BLK_WB_LDS 2
 #endif
@@ -131,19 +140,41 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     };
     // the dot block (id, rd) of the next pass, chunks < PFX, into lpf by global_load_lds
     // (dummy slots load the block's first real column: finite values for h = 0)
-    auto prefetch = [&](int id, int rd) {
+    // kpoll < NW (during an all-gather whose K values are polled by waves 0 .. K-1, on N
+    // ranks the rank-total pushers among them): the waves kpoll .. NW-1 load every wave's
+    // elements, so the polls -- and a pusher's push -- do not wait, in their wave's vmcnt
+    // order, for the prefetch to land; the barrier after the all-gather hands the LDS over
+    auto prefetch = [&](int id, int rd, int kpoll) {
         if constexpr (PFX > 0) {
             int cb, ce;
             range(cb, ce);
+            const int nd = NW - kpoll, wd = wv - kpoll;
+            if (kpoll >= NW) {
 #pragma unroll
-            for (int d = 0; d < S; ++d) {
-                const int qd = d - (S - rd);
-                const double2 *D = V2 + (i64)(id + (qd > 0 ? qd : 0)) * ld2;
+                for (int d = 0; d < S; ++d) {
+                    const int qd = d - (S - rd);
+                    const double2 *D = V2 + (i64)(id + (qd > 0 ? qd : 0)) * ld2;
 #pragma unroll
-                for (int k = 0; k < PFX; ++k)
-                    if (cb + k < ce)
-                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(at(D, cb + k)),
-                                                         (lds_void_t *)(lpf + (d * PFX + k) * NT + (t & ~63)), 16, 0, 0);
+                    for (int k = 0; k < PFX; ++k)
+                        if (cb + k < ce)
+                            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(at(D, cb + k)),
+                                                             (lds_void_t *)(lpf + (d * PFX + k) * NT + (t & ~63)), 16, 0,
+                                                             0);
+                }
+            } else if (wd >= 0) {
+                for (int g = wd; g < NW; g += nd)  // element group g (64 elements) of every chunk
+#pragma unroll
+                    for (int d = 0; d < S; ++d) {
+                        const int qd = d - (S - rd);
+                        const double2 *D = V2 + (i64)(id + (qd > 0 ? qd : 0)) * ld2 + g * 64;
+#pragma unroll
+                        for (int k = 0; k < PFX; ++k)
+                            if (cb + k < ce)
+                                __builtin_amdgcn_global_load_lds(
+                                    reinterpret_cast<const void *>(reinterpret_cast<const char *>(D + (i64)(cb + k) * NT) +
+                                                                   lane * 16),
+                                    (lds_void_t *)(lpf + (d * PFX + k) * NT + g * 64), 16, 0, 0);
+                    }
             }
         }
     };
@@ -169,7 +200,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
     }
     for (int k = 0; k < LW; ++k)
         if (l0 + k < lend) lw[k * NT + t] = W2[(l0 + k) * NT + t];
-    prefetch(blk_lo(blk_of(1), S), blk_n(blk_of(1), S, j));  // pass 0's dot block
+    prefetch(blk_lo(blk_of(1), S), blk_n(blk_of(1), S, j), NW);  // pass 0's dot block
     // h of block 0 = <w, V(:,1)>: the operator launch's partial slab (on N ranks
     // its rank hop here, res_pin_fold)
     double h;
@@ -390,7 +421,7 @@ __global__ __launch_bounds__(NT, 1) void k_mgs_blk(ResArgs a) {
         }
         if (p + 2 < P) {  // the next pass reduces dots: its block's loads overlap this all-gather
             const int b2 = blk_of(p + 2);
-            prefetch(blk_lo(b2, S), blk_n(b2, S, j));
+            prefetch(blk_lo(b2, S), blk_n(b2, S, j), BLK_PF_SPLIT && S == 1 ? K : NW);
         }
         for (int v = wv; v < vend; v += NW) {
             double out = 0.0;

@@ -75,7 +75,8 @@ def compare(lines: list[dict], pred: dict) -> list[dict]:
                      "collective_latency_us": d.get("collective_latency_us"),
                      "blocked_it_s": bl.get("it_s"), "blocked_S": bl.get("projection_block"),
                      "blocked_predicted_it_s": bp.get("predicted_it_s"),
-                     "blocked_verdict": _band(bl.get("it_s"), bp.get("predicted_it_s"))})
+                     "blocked_verdict": _band(bl.get("it_s"), bp.get("predicted_it_s")),
+                     "strict_prefetch_it_s": (d.get("strict_prefetch_leg") or {}).get("it_s")})
     return rows
 
 
@@ -86,12 +87,13 @@ def main() -> None:
     a = ap.parse_args()
     rows = compare(bench_lines(json.load(open(a.scale))), json.load(open(a.pred)))
     print("| N | it/s | predicted | verdict | variant | collective | wait us (pred) | collective us |"
-          " blocked leg it/s (S) | predicted | verdict |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|")
+          " blocked leg it/s (S) | predicted | verdict | strict-prefetch leg it/s |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     for r in rows:
         print(f"| {r['n_gpus']} | {r['it_s']} | {r['predicted_it_s']} | {r['verdict']} | {r['variant']} | "
               f"{r['collective']} | {r['wait_us']} ({r['predicted_wait_us']}) | {r['collective_latency_us']} | "
-              f"{r['blocked_it_s']} ({r['blocked_S']}) | {r['blocked_predicted_it_s']} | {r['blocked_verdict']} |")
+              f"{r['blocked_it_s']} ({r['blocked_S']}) | {r['blocked_predicted_it_s']} | {r['blocked_verdict']} | "
+              f"{r['strict_prefetch_it_s']} |")
 
 
 if __name__ == "__main__":
