@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5, last tree: the whole GPU suite, smoke and the default bench line.
-OUT=gpurun_out/r05zz
+OUT=gpurun_out/${TAG:-r05zz}
 cd "$GRAFT_REPO_ROOT" || exit 1
 source tools/gpu_lib.sh
 export PYTHONUNBUFFERED=1
