@@ -8,7 +8,7 @@ restart loop and the Givens rotations.
 """
 from ._native import GkError, runtime_info
 from .solver import (MGSR_MF, MGSR_OMP, PREC, Context, LocalGroup, SolveResult, gmres_hh, gmres_mgsr, pbicgstab,
-                     pcg, res_plan_query, slab_partition)
+                     SrSolve, pcg, res_plan_query, slab_partition)
 
 __all__ = ["GkError", "Context", "LocalGroup", "SolveResult", "gmres_mgsr", "gmres_hh", "slab_partition", "pcg", "pbicgstab", "MGSR_OMP", "MGSR_MF", "PREC",
-           "res_plan_query", "runtime_info"]
+           "res_plan_query", "runtime_info", "SrSolve"]

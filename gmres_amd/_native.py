@@ -43,7 +43,12 @@ GK_TUNE_RES_PF = 27
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 (GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES, GK_KID_PREC,
  GK_KID_HALO, GK_KID_GRAPH) = range(10)
-KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res", "prec", "halo", "graph"]
+# short-recurrence passes (GK_KID_SR + pass kind, gmres_amd/csrc/gk_sr.hpp)
+GK_KID_SR = 10
+SR_PASS_NAMES = ["sr_cg_p", "sr_cg_x", "sr_cg_z", "sr_bi_p", "sr_bi_pc", "sr_bi_s", "sr_bi_sc", "sr_st1", "sr_st2",
+                 "sr_bi_x", "sr_bi_pe", "sr_bi_se", "sr_dot"]
+KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res", "prec", "halo", "graph"] + SR_PASS_NAMES
+GK_SR_PCG, GK_SR_BICGSTAB = 0, 1
 COMM_KINDS = {0: None, 1: "rccl", 2: "local-group", 3: "xgmi-device-exchange"}
 # resident-step variants (gk_res_info / gk_res_plan_query)
 RES_VARIANTS = {0: None, 1: "prefetch", 2: "pairs", 3: "pairs+lds", 4: "w-only", 5: "w+column", 6: "blocked"}
@@ -125,6 +130,10 @@ _SIGS = {
     "gk_vec_apply": (c_int, [c_vp, c_int, c_int, c_int]),
     "gk_vec_dot": (c_int, [c_vp, c_int, c_int, _dp]),
     "gk_vec_lincomb": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_double, c_double]),
+    "gk_sr_start": (c_int, [c_vp, c_int, c_double, c_int]),
+    "gk_sr_iterate": (c_int, [c_vp, c_int]),
+    "gk_sr_status": (c_int, [c_vp, c_int, _ip, _ip, _dp]),
+    "gk_sr_history": (c_int, [c_vp, _dp, c_int]),
     "gk_poisson5": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "gk_precond_apply": (c_int, [c_int, c_int, _dp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "gk_mgs_project": (c_int, [c_ll, c_vp, c_vp, c_vp, c_vp]),
@@ -134,6 +143,7 @@ _SIGS = {
 _FSIGS = {
     "pcg_hip_run": (c_int, [c_vp, c_double, _ip, _dp, c_int, _dp]),
     "pbicgstab_hip_run": (c_int, [c_vp, c_double, _ip, _dp, c_int, _dp]),
+    "sr_hip_run_seq": (c_int, [c_vp, c_int, c_double, _ip, _dp, c_int, _dp]),
     "gmres_mgsr_hip_run": (c_int, [c_vp, c_int, c_double, c_int, c_int, _dp, _dp, _dp, _ip, _ip, c_int, c_int,
                                    _dp, _dp, _ip, c_int]),
     "gmres_hh_hip_run": (c_int, [c_vp, c_int, c_double, c_int, c_int, c_int, _dp, _dp, _dp, _ip, _ip, c_int,

@@ -36,7 +36,7 @@ HIP_UNITS = ([(HIP_SOURCES[0], [], "gk_api.o")] + [(HIP_SOURCES[1], [f"GK_CF_PAR
                                                     for p in range(GK_CF_PARTS)]
              + [(HIP_SOURCES[2], [], "gk_blk.o")])
 HIP_HEADERS = [os.path.join(CSRC, h) for h in ("gk_common.hpp", "gk_kernels.hpp", "gk_cheb.hpp", "gk_res.hpp",
-                                                "gk_blk.hpp")]
+                                                "gk_blk.hpp", "gk_sr.hpp")]
 HIP_DEPS = HIP_SOURCES + HIP_HEADERS + [os.path.join(ROOT, "include", "gmres_hip.h")]
 HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
 F_SOURCES = [os.path.join(FSRC, "gmres_hip.f90")]

@@ -21,12 +21,14 @@
 #include <mutex>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <string>
 #include <vector>
 
 #include "../../include/gmres_hip.h"
 #include "gk_blk.hpp"
 #include "gk_kernels.hpp"
+#include "gk_sr.hpp"
 
 using gk::i64;
 
@@ -190,6 +192,15 @@ struct gk_ctx {
     int nev = 0;
     double prof_ms[GK_NKID] = {0};
     long long prof_n[GK_NKID] = {0};
+    // fused short-recurrence solve (gk_sr_*)
+    gk::SrDev *sr_dev = nullptr;
+    gk::SrMirror *sr_mir = nullptr, *sr_mir_dev = nullptr;  // mapped pinned
+    double *sr_hist = nullptr;
+    int sr_hist_len = 0;
+    int sr_solver = -1, sr_par = 0, sr_queued = 0, sr_maxit = 0;
+    std::deque<hipEvent_t> sr_pend;   // end of each queued chunk, oldest first
+    std::vector<hipEvent_t> sr_evfree;
+    hipGraphExec_t sr_graph = nullptr;  // SR_GRAPH_ITERS iterations from parity 0
 };
 
 namespace {
@@ -235,6 +246,10 @@ void graph_reset(gk_ctx *c) {
             g = nullptr;
         }
     c->gkey = -1;
+    if (c->sr_graph != nullptr) {
+        (void)hipGraphExecDestroy(c->sr_graph);
+        c->sr_graph = nullptr;
+    }
 }
 
 // ----------------------------------------------------------------- comm ---
@@ -1727,6 +1742,11 @@ int gk_destroy(gk_ctx *c) {
     if (c->res_stamps) (void)hipFree(c->res_stamps);
     if (c->res_trace) (void)hipFree(c->res_trace);
     if (c->res_err) (void)hipHostFree(c->res_err);
+    if (c->sr_dev) (void)hipFree(c->sr_dev);
+    if (c->sr_mir) (void)hipHostFree(c->sr_mir);
+    if (c->sr_hist) (void)hipFree(c->sr_hist);
+    for (hipEvent_t e : c->sr_pend) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->sr_evfree) (void)hipEventDestroy(e);
     double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi, c->dh,
                       c->red, c->hcol, c->ydev, c->hb, c->scal, c->Vb, c->gram_slab, c->gram_out};
     for (double *p : bufs)
@@ -3094,6 +3114,398 @@ int gk_vec_lincomb(gk_ctx *c, int form, int out, int a, int b, int cc, double s1
     gk::k_lincomb<<<c->nblk_stream, gk::TPB, 0, c->st>>>(form, vo, va, vb, vc, s1, s2, c->nloc);
     LAUNCHCHK();
     return GK_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------- fused short-recurrence solvers -------
+// pcg_omp (src/cg.f90:154-234) and pbicgstab_omp (src/bicgstab.f90:91-182) with
+// every scalar on the device (gk_sr.hpp).  Vectors: Krylov columns 0..7 and the
+// work vectors w, vj (free between GMRES cycles).  p and ap alternate between two
+// buffers by iteration parity: the line march reads them with their neighbour
+// lines while it writes the next ones.
+
+namespace {
+constexpr int SR_GRAPH_ITERS = 16;  // iterations per captured graph (even: the parity returns to 0)
+
+struct SrVecs {
+    double *r, *z, *r0, *p[2], *ap[2], *s, *as, *z1, *z2;
+};
+
+SrVecs sr_vecs(gk_ctx *c) {
+    auto col = [&](int k) { return c->V + (i64)k * c->ld; };
+    SrVecs v{};
+    v.r = col(0);
+    v.z = col(1);   // PCG
+    v.r0 = col(1);  // BiCGSTAB
+    v.p[0] = col(2);
+    v.p[1] = col(3);
+    v.ap[0] = col(4);
+    v.ap[1] = col(5);
+    v.s = col(6);
+    v.as = col(7);
+    v.z1 = c->w;
+    v.z2 = c->vj;
+    return v;
+}
+
+bool sr_slabs(const gk_ctx *c) { return collective(c) && c->nranks > 1; }
+
+gk::SrArgs sr_args(gk_ctx *c) {
+    gk::SrArgs a{};
+    a.sd = c->sr_dev;
+    a.hist = c->sr_hist;
+    a.mir = c->sr_mir_dev;
+    a.part0 = slot(c, 0);
+    a.part1 = slot(c, 1);
+    a.N = c->N;
+    a.nlines = c->nlines;
+    a.JT = c->JT;
+    // cbpr2 coefficients exactly as chebyshev.f90:19-25 (precond_sweeps)
+    const double cc = (c->p1 - c->p0) / 2.0, d = (c->p1 + c->p0) / 2.0;
+    double al = 1.0 / d;
+    double be = cc * al / 2.0;
+    be = be * be;
+    al = 1.0 / (d - be);
+    a.cd = d;
+    a.ca = al;
+    return a;
+}
+
+// N ranks: the partial slab(s) are all-reduced, then k_sr_fin runs the finaliser.
+int sr_fin_after(gk_ctx *c, int fin, int np, bool two) {
+    if (fin == gk::FIN_NONE) return GK_OK;
+    if (sr_slabs(c)) {
+        CHK(allreduce(c, slot(c, 0), np));
+        if (two) CHK(allreduce(c, slot(c, 1), np));
+    }
+    gk::k_sr_fin<<<1, gk::TPB, 0, c->st>>>(fin, c->sr_dev, slot(c, 0), slot(c, 1), np, c->sr_hist, c->sr_mir_dev);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
+template <int K>
+int sr_march(gk_ctx *c, gk::SrArgs a, int fin) {
+    constexpr int NIN = gk::sr_nin<K>();
+    const bool slabs = sr_slabs(c);
+    if (slabs) {  // one halo line of every operand input (the operand is formed on load)
+        const bool has_lo = c->rank > 0, has_hi = c->rank < c->nranks - 1;
+        const double *in[3] = {a.in0, a.in1, a.in2};
+        for (int v = 0; v < NIN; ++v) {
+            double *lo = c->dh + (i64)(2 * v) * gk::CF_HMAX * c->N;
+            double *hi = c->dh + (i64)(2 * v + 1) * gk::CF_HMAX * c->N;
+            CHK(halo_lines(c, in[v], 1, lo, hi));
+            a.lo[v] = has_lo ? lo : nullptr;
+            a.hi[v] = has_hi ? hi : nullptr;
+        }
+    }
+    a.fin = slabs ? gk::FIN_NONE : fin;
+    {
+        ProfScope ps(c, GK_KID_SR + K);
+        if (c->vec == 2)
+            gk::k_sr_march<2, K><<<c->sgrid, gk::TPB, 0, c->st>>>(a);
+        else
+            gk::k_sr_march<1, K><<<c->sgrid, gk::TPB, 0, c->st>>>(a);
+        LAUNCHCHK();
+    }
+    if (slabs) CHK(sr_fin_after(c, fin, c->np_st, gk::sr_nacc<K>() > 1));
+    return GK_OK;
+}
+
+template <int K>
+int sr_vec(gk_ctx *c, gk::SrArgs a, int fin) {
+    const bool slabs = sr_slabs(c);
+    a.fin = slabs ? gk::FIN_NONE : fin;
+    {
+        ProfScope ps(c, GK_KID_SR + 9 + K);
+        // the grid (hence the partial count) comes from the largest slab: the same on every rank
+        gk::k_sr_vec<K, 4><<<c->np_pj, gk::TPB, 0, c->st>>>(a, c->nloc);
+        LAUNCHCHK();
+    }
+    if (slabs) CHK(sr_fin_after(c, fin, c->np_pj, K == gk::SRV_BI_X));
+    return GK_OK;
+}
+
+// out = M^-1 in by the generic preconditioner sweeps (Chebyshev(k)); with vdot
+// the last sweep's dot <out, vdot> feeds finaliser `fin`.
+int sr_prec(gk_ctx *c, const double *in, double *out, const double *vdot, int fin) {
+    double *keep = c->z;
+    c->z = const_cast<double *>(in);  // precond_sweeps reads its input from c->z
+    const int rc = precond_sweeps(c, out, vdot != nullptr ? gk::ACC_DOT : gk::ACC_NONE, vdot, slot(c, 0));
+    c->z = keep;
+    CHK(rc);
+    if (fin == gk::FIN_NONE) return GK_OK;
+    return sr_fin_after(c, fin, c->last_np, false);
+}
+
+// One PCG iteration (cg.f90:188-232) from parity par.
+int sr_pcg_iter(gk_ctx *c, int par) {
+    const SrVecs v = sr_vecs(c);
+    const bool id = c->pkind == GK_PREC_IDENTITY;
+    gk::SrArgs a = sr_args(c);
+    // p = z + beta p ; alpha = rz / <A p, p>
+    a.in0 = id ? v.r : v.z;
+    a.in1 = v.p[par];
+    a.ou = v.p[par ^ 1];
+    CHK(sr_march<gk::SRK_CG_P>(c, a, gk::FIN_CG_ALPHA));
+    // x += alpha p ; r -= alpha A p ; res = ||r|| (identity: beta = <r,r> / rz)
+    a = sr_args(c);
+    a.in0 = v.p[par ^ 1];
+    a.x = c->x;
+    a.r = v.r;
+    CHK(sr_march<gk::SRK_CG_X>(c, a, id ? gk::FIN_CG_RES_ID : gk::FIN_CG_RES));
+    if (id) return GK_OK;
+    // z = M^-1 r ; beta = <r, z> / rz
+    if (c->pkind == GK_PREC_CBPR2) {
+        a = sr_args(c);
+        a.in0 = v.r;
+        a.oy = v.z;
+        return sr_march<gk::SRK_CG_Z>(c, a, gk::FIN_CG_BETA);
+    }
+    return sr_prec(c, v.r, v.z, v.r, gk::FIN_CG_BETA);
+}
+
+// One BiCGSTAB iteration (bicgstab.f90:120-180) from parity par.
+int sr_bicg_iter(gk_ctx *c, int par) {
+    const SrVecs v = sr_vecs(c);
+    const int pk = c->pkind;
+    double *pn = v.p[par ^ 1], *apn = v.ap[par ^ 1];
+    const double *z1 = pn, *z2 = v.s;
+    // p = r + beta (p - omega ap) ; z1 = M^-1 p ; ap = A z1 ; alpha = rr0 / <ap, r0>
+    gk::SrArgs a = sr_args(c);
+    a.in0 = v.r;
+    a.in1 = v.p[par];
+    a.in2 = v.ap[par];
+    a.ou = pn;
+    if (pk == GK_PREC_IDENTITY) {
+        a.oy = apn;
+        a.vd = v.r0;
+        CHK(sr_march<gk::SRK_BI_P>(c, a, gk::FIN_BI_ALPHA));
+    } else {
+        z1 = v.z1;
+        z2 = v.z2;
+        if (pk == GK_PREC_CBPR2) {
+            a.oy = v.z1;
+            CHK(sr_march<gk::SRK_BI_PC>(c, a, gk::FIN_NONE));
+        } else {
+            CHK(sr_vec<gk::SRV_BI_PE>(c, a, gk::FIN_NONE));
+            CHK(sr_prec(c, pn, v.z1, nullptr, gk::FIN_NONE));
+        }
+        a = sr_args(c);
+        a.in0 = v.z1;
+        a.oy = apn;
+        a.vd = v.r0;
+        CHK(sr_march<gk::SRK_ST1>(c, a, gk::FIN_BI_ALPHA));
+    }
+    // s = r - alpha ap ; z2 = M^-1 s ; as = A z2 ; omega = <as, s> / <as, as>
+    a = sr_args(c);
+    a.in0 = v.r;
+    a.in1 = apn;
+    a.ou = v.s;
+    if (pk == GK_PREC_IDENTITY) {
+        a.oy = v.as;
+        CHK(sr_march<gk::SRK_BI_S>(c, a, gk::FIN_BI_OMEGA));
+    } else {
+        if (pk == GK_PREC_CBPR2) {
+            a.oy = v.z2;
+            CHK(sr_march<gk::SRK_BI_SC>(c, a, gk::FIN_NONE));
+        } else {
+            CHK(sr_vec<gk::SRV_BI_SE>(c, a, gk::FIN_NONE));
+            CHK(sr_prec(c, v.s, v.z2, nullptr, gk::FIN_NONE));
+        }
+        a = sr_args(c);
+        a.in0 = v.z2;
+        a.oy = v.as;
+        a.vd = v.s;
+        CHK(sr_march<gk::SRK_ST2>(c, a, gk::FIN_BI_OMEGA));
+    }
+    // x = x + alpha z1 + omega z2 ; r = s - omega as ; res, beta
+    a = sr_args(c);
+    a.x = c->x;
+    a.r = v.r;
+    a.in0 = z1;
+    a.in1 = z2;
+    a.in2 = v.s;
+    a.e0 = v.as;
+    a.vd = v.r0;
+    return sr_vec<gk::SRV_BI_X>(c, a, gk::FIN_BI_RES);
+}
+
+int sr_iter(gk_ctx *c, int par) { return c->sr_solver == GK_SR_PCG ? sr_pcg_iter(c, par) : sr_bicg_iter(c, par); }
+
+// Capture SR_GRAPH_ITERS iterations from parity 0 as one graph (single rank; a
+// capture that fails leaves the eager path).
+int sr_capture(gk_ctx *c) {
+    HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+    c->capturing = true;
+    int rc = GK_OK;
+    for (int i = 0; i < SR_GRAPH_ITERS && rc == GK_OK; ++i) rc = sr_iter(c, i & 1);
+    c->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(c->st, &g);
+    hipGraphExec_t ge = nullptr;
+    hipError_t e2 = hipErrorUnknown;
+    if (rc == GK_OK && e == hipSuccess && g != nullptr) e2 = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    if (g != nullptr) (void)hipGraphDestroy(g);
+    if (rc != GK_OK || e != hipSuccess || e2 != hipSuccess) {
+        (void)hipGetLastError();
+        if (ge != nullptr) (void)hipGraphExecDestroy(ge);
+        return set_err(GK_ERR_HIP, "capture of the short-recurrence iterations failed (%s)",
+                       rc != GK_OK ? g_err.c_str() : hipGetErrorString(e != hipSuccess ? e : e2));
+    }
+    c->sr_graph = ge;
+    return GK_OK;
+}
+
+void sr_recycle(gk_ctx *c, hipEvent_t e) { c->sr_evfree.push_back(e); }
+
+int sr_drain(gk_ctx *c) {
+    if (c->sr_pend.empty()) return GK_OK;
+    const int rc = sync_st(c);
+    for (hipEvent_t e : c->sr_pend) sr_recycle(c, e);
+    c->sr_pend.clear();
+    return rc;
+}
+
+int sr_start_body(gk_ctx *c, int solver) {
+    const SrVecs v = sr_vecs(c);
+    const size_t vb = sizeof(double) * (size_t)c->nloc;
+    HIPCHK(hipMemsetAsync(c->x, 0, vb, c->st));
+    HIPCHK(hipMemcpyAsync(v.r, c->b, vb, hipMemcpyDeviceToDevice, c->st));
+    gk::SrArgs a = sr_args(c);
+    if (solver == GK_SR_PCG) {
+        HIPCHK(hipMemsetAsync(v.p[0], 0, vb, c->st));  // iteration 1: p = z + 0 * 0 = z  (cg.f90:183-187)
+        if (c->pkind == GK_PREC_IDENTITY) {
+            a.in0 = v.r;
+            a.in1 = v.r;
+            return sr_vec<gk::SRV_DOT>(c, a, gk::FIN_CG_INIT);
+        }
+        if (c->pkind == GK_PREC_CBPR2) {
+            a.in0 = v.r;
+            a.oy = v.z;
+            return sr_march<gk::SRK_CG_Z>(c, a, gk::FIN_CG_INIT);
+        }
+        return sr_prec(c, v.r, v.z, v.r, gk::FIN_CG_INIT);
+    }
+    // r0 = p = r (bicgstab.f90:112-118); iteration 1: p = r + 0 (p - 1 * 0) = r
+    HIPCHK(hipMemcpyAsync(v.r0, c->b, vb, hipMemcpyDeviceToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(v.p[0], c->b, vb, hipMemcpyDeviceToDevice, c->st));
+    HIPCHK(hipMemsetAsync(v.ap[0], 0, vb, c->st));
+    a.in0 = v.r;
+    a.in1 = v.r0;
+    return sr_vec<gk::SRV_DOT>(c, a, gk::FIN_BI_INIT);
+}
+}  // namespace
+
+extern "C" {
+
+int gk_sr_start(gk_ctx *c, int solver, double tol, int max_iter) {
+    CHK(check_ctx(c));
+    if (solver != GK_SR_PCG && solver != GK_SR_BICGSTAB) return set_err(GK_ERR_ARG, "bad solver %d", solver);
+    if (max_iter < 0 || max_iter > (1 << 28)) return set_err(GK_ERR_ARG, "bad max_iter %d", max_iter);
+    if (c->m < 7) return set_err(GK_ERR_ARG, "short-recurrence solvers need a context with m >= 7 (vectors)");
+    HIPCHK(hipSetDevice(c->dev));
+    CHK(sr_drain(c));
+    c->cycle_mgs = c->cycle_hh = false;  // the Krylov columns are the solver's vectors now
+    if (c->sr_dev == nullptr) {
+        HIPCHK(hipMalloc(&c->sr_dev, sizeof(gk::SrDev)));
+        HIPCHK(hipHostMalloc((void **)&c->sr_mir, sizeof(gk::SrMirror), hipHostMallocMapped));
+        HIPCHK(hipHostGetDevicePointer((void **)&c->sr_mir_dev, c->sr_mir, 0));
+    }
+    if (c->sr_hist_len < std::max(max_iter, 1)) {
+        if (c->sr_hist != nullptr) (void)hipFree(c->sr_hist);
+        c->sr_hist = nullptr;
+        c->sr_hist_len = 0;
+        HIPCHK(hipMalloc(&c->sr_hist, sizeof(double) * (size_t)std::max(max_iter, 1)));
+        c->sr_hist_len = std::max(max_iter, 1);
+        graph_reset(c);  // a captured graph holds the old history pointer
+    }
+    if (c->sr_solver != solver && c->sr_graph != nullptr) {
+        (void)hipGraphExecDestroy(c->sr_graph);
+        c->sr_graph = nullptr;
+    }
+    c->sr_solver = solver;
+    c->sr_par = 0;
+    c->sr_queued = 0;
+    c->sr_maxit = max_iter;
+    gk::SrDev d{};
+    d.omega = 1.0;
+    d.tol = tol;
+    d.maxit = max_iter;
+    HIPCHK(hipMemcpyAsync(c->sr_dev, &d, sizeof d, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));  // d is a stack object
+    c->sr_mir->it = 0;
+    c->sr_mir->done = 0;
+    c->sr_mir->res = 0.0;
+    return sr_start_body(c, solver);
+}
+
+int gk_sr_iterate(gk_ctx *c, int k) {
+    CHK(check_ctx(c));
+    if (c->sr_solver < 0) return set_err(GK_ERR_STATE, "gk_sr_iterate before gk_sr_start");
+    if (k < 0 || (long long)c->sr_queued + k > c->sr_maxit)
+        return set_err(GK_ERR_ARG, "gk_sr_iterate(%d): beyond max_iter %d (%d queued)", k, c->sr_maxit, c->sr_queued);
+    if (k == 0) return GK_OK;
+    HIPCHK(hipSetDevice(c->dev));
+    const bool graphs = c->tune_graph != 0 && !collective(c) && !c->prof;
+    int left = k;
+    while (left > 0) {
+        if (graphs && c->sr_par == 0 && left >= SR_GRAPH_ITERS) {
+            if (c->sr_graph == nullptr) CHK(sr_capture(c));
+            HIPCHK(hipGraphLaunch(c->sr_graph, c->st));
+            left -= SR_GRAPH_ITERS;
+            c->sr_queued += SR_GRAPH_ITERS;
+            continue;
+        }
+        CHK(sr_iter(c, c->sr_par));
+        c->sr_par ^= 1;
+        --left;
+        ++c->sr_queued;
+    }
+    hipEvent_t e = nullptr;
+    if (!c->sr_evfree.empty()) {
+        e = c->sr_evfree.back();
+        c->sr_evfree.pop_back();
+    } else {
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    HIPCHK(hipEventRecord(e, c->st));
+    c->sr_pend.push_back(e);
+    return GK_OK;
+}
+
+int gk_sr_status(gk_ctx *c, int wait, int *executed, int *done, double *res) {
+    CHK(check_ctx(c));
+    if (c->sr_solver < 0) return set_err(GK_ERR_STATE, "gk_sr_status before gk_sr_start");
+    HIPCHK(hipSetDevice(c->dev));
+    if (wait == 0 && !c->sr_pend.empty()) {
+        hipEvent_t e = c->sr_pend.front();
+        c->sr_pend.pop_front();
+        const int rc = spin_until(c, query_event, e, "short-recurrence chunk");
+        sr_recycle(c, e);
+        CHK(rc);
+        CHK(res_check(c));
+        CHK(xs_check(c));
+    } else {
+        CHK(sr_drain(c));
+        CHK(sync_st(c));
+    }
+    if (c->prof) CHK(prof_harvest(c));
+    if (executed) *executed = __atomic_load_n(&c->sr_mir->it, __ATOMIC_ACQUIRE);
+    if (done) *done = __atomic_load_n(&c->sr_mir->done, __ATOMIC_ACQUIRE);
+    if (res) *res = *(volatile double *)&c->sr_mir->res;
+    return GK_OK;
+}
+
+int gk_sr_history(gk_ctx *c, double *hist, int n) {
+    CHK(check_ctx(c));
+    if (c->sr_solver < 0) return set_err(GK_ERR_STATE, "gk_sr_history before gk_sr_start");
+    if (n < 0 || n > c->sr_hist_len || hist == nullptr) return set_err(GK_ERR_ARG, "bad history length %d", n);
+    HIPCHK(hipSetDevice(c->dev));
+    CHK(sr_drain(c));
+    if (n == 0) return GK_OK;
+    HIPCHK(hipMemcpyAsync(hist, c->sr_hist, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
+    return sync_st(c);
 }
 
 }  // extern "C"

@@ -1,0 +1,416 @@
+// gk_sr.hpp -- fused device passes of the short-recurrence solvers that share
+// the GMRES operator / preconditioner seam: pcg_omp (src/cg.f90:154-234) and
+// pbicgstab_omp (src/bicgstab.f90:91-182).
+//
+// The reference runs every BLAS-1 operation as its own OpenMP loop and keeps
+// the scalars (alpha, beta, omega, the residual) in `single` blocks.  Here one
+// iteration is two (PCG, identity) to five (BiCGSTAB, cbpr2) passes over HBM:
+//
+//   * k_sr_march: a Poisson-5 line march (k_stencil's register scheme: lines
+//     j-1, j, j+1 in registers, W/E neighbours by __shfl) whose OPERAND is
+//     formed on load from up to three vectors -- p = z + beta p, p = r +
+//     beta (p - omega ap), s = r - alpha ap -- so the vector update that
+//     precedes a stencil in the reference costs no pass of its own, and whose
+//     epilogue carries the element-wise updates and dots that follow it;
+//   * k_sr_vec: the element-wise passes (BiCGSTAB's x / r update with its two
+//     dots), double2 streams.
+//
+// Scalars never leave the device.  Every pass writes one partial per
+// workgroup; the LAST workgroup to finish (a completion ticket, one atomic per
+// workgroup) sums the slab in a fixed order and computes the next scalar
+// (alpha = rz / <Ap, p>, ...) into SrDev, which the next pass reads.  On N
+// ranks the slab is all-reduced first and k_sr_fin does the same on one
+// workgroup.  The per-iteration residual goes to a device history and a
+// mapped host mirror; once it drops below tol every later pass returns at
+// entry -- the reference's `if (converged) cycle` -- so the host may queue
+// iterations ahead without reading anything back per iteration.
+//
+// Element-wise expressions keep the reference's association order (compiled
+// with -ffp-contract=off); only the dot-product summation order differs.
+#pragma once
+#include "gk_kernels.hpp"  // ld_vec, st_vec
+
+namespace gk {
+
+// Device-resident scalars of one short-recurrence solve.
+struct SrDev {
+    double rz;      // PCG: <r, z> of the current iteration; BiCGSTAB: rr0 = <r, r0>
+    double alpha, beta, omega;
+    double res;     // residual of the last executed iteration
+    double tol;
+    int it;         // iterations executed
+    int done;       // first iteration with res < tol (0: none)
+    unsigned ticket;  // completion ticket of the running pass (0 between passes)
+    int maxit;      // length of the history
+};
+
+// Mapped host copy, written by the residual finaliser of every iteration.
+struct SrMirror {
+    int it, done;
+    double res;
+};
+
+// Fused line-march passes.  Operand u per point; t = u / d for the cbpr2
+// passes (chebyshev.f90:27-31), else t = u; ax = A t.
+enum {
+    SRK_CG_P = 0,  // u = z + beta p (cg.f90:227-231); ou = u; dot <A u, u> (:196-199)
+    SRK_CG_X = 1,  // u = p; x += alpha u; r -= alpha A u; dot <r, r> (:206-211)
+    SRK_CG_Z = 2,  // u = r; oy = z = cbpr2(r) (chebyshev.f90:27-37); dot <r, z> (cg.f90:213-217)
+    SRK_BI_P = 3,  // u = r + beta (p - omega ap) (bicgstab.f90:176-180); ou = u; oy = ap = A u; dot <ap, r0>
+    SRK_BI_PC = 4, // u as BI_P; ou = u; oy = z1 = cbpr2(u)
+    SRK_BI_S = 5,  // u = s = r - alpha ap (:131-135); ou = s; oy = as = A s; dots <as, s>, <as, as> (:139-144)
+    SRK_BI_SC = 6, // u as BI_S; ou = s; oy = z2 = cbpr2(s)
+    SRK_ST1 = 7,   // u = in0; oy = A u; dot <A u, vd>        (cbpr2 BiCGSTAB: ap = A z1, <ap, r0>)
+    SRK_ST2 = 8,   // u = in0; oy = A u; dots <A u, vd>, <A u, A u>  (as = A z2, <as, s>, <as, as>)
+};
+
+// Element-wise passes.
+enum {
+    SRV_BI_X = 0,   // x = (x + alpha z1) + omega z2; r = s - omega as; dots <r, r>, <r, r0> (:148-171)
+    SRV_BI_PE = 1,  // ou = r + beta (p - omega ap)          (generic preconditioner)
+    SRV_BI_SE = 2,  // ou = r - alpha ap                     (generic preconditioner)
+    SRV_DOT = 3,    // dot <in0, in1>                         (solve start)
+};
+
+// What the last workgroup computes from the pass's partial slab(s).
+enum {
+    FIN_NONE = 0,
+    FIN_CG_INIT = 1,   // rz = <r, z>; beta = 0 (p = z + 0 * 0 on the first iteration)
+    FIN_CG_ALPHA = 2,  // alpha = rz / <Ap, p>                          (cg.f90:200-202)
+    FIN_CG_RES_ID = 3, // identity M: res = sqrt(<r,r>); beta = <r,r> / rz; rz = <r,r>  (:218-226)
+    FIN_CG_RES = 4,    // res = sqrt(<r,r>) (beta from FIN_CG_BETA)
+    FIN_CG_BETA = 5,   // beta = <r, z> / rz; rz = <r, z>
+    FIN_BI_INIT = 6,   // rr0 = <r, r0>; beta = 0; omega = 1
+    FIN_BI_ALPHA = 7,  // alpha = rr0 / <ap, r0>                        (:127-129)
+    FIN_BI_OMEGA = 8,  // omega = <as, s> / <as, as>                   (:145-147)
+    FIN_BI_RES = 9,    // res = sqrt(<r,r>); beta = (<r,r0> / rr0) (alpha / omega); rr0 = <r,r0>  (:159-175)
+};
+
+struct SrArgs {
+    const double *in0, *in1, *in2;  // operand inputs (k_sr_march) / element-wise inputs (k_sr_vec)
+    const double *lo[3], *hi[3];    // halo line of each operand input (nullptr: physical boundary)
+    double *ou;                     // the operand u itself (p, s)
+    double *oy;                     // the stencil output (ap, as, z, z1, z2)
+    double *x, *r;                  // updated in place (CG_X; BI_X)
+    const double *e0;               // BI_X: as
+    const double *vd;               // dot partner (r0, s)
+    double *part0, *part1;          // partial slabs (one entry per workgroup)
+    SrDev *sd;
+    double *hist;                   // device history [maxit]
+    SrMirror *mir;                  // mapped host mirror
+    double cd, ca;                  // cbpr2: d, alpha (chebyshev.f90:19-25)
+    int N, nlines, JT, fin;
+};
+
+// The finaliser: one workgroup (all TPB threads) after every partial of the
+// pass is visible.
+__device__ __forceinline__ void sr_fin(int mode, SrDev *sd, const double *p0, const double *p1, int np,
+                                       double *hist, SrMirror *mir, double *sm) {
+    const double s0 = reduce_slab(p0, np, sm);
+    const double s1 = (mode == FIN_BI_OMEGA || mode == FIN_BI_RES) ? reduce_slab(p1, np, sm) : 0.0;
+    if (threadIdx.x != 0) return;
+    switch (mode) {
+        case FIN_CG_INIT:
+            sd->rz = s0;
+            sd->beta = 0.0;
+            break;
+        case FIN_CG_ALPHA: sd->alpha = sd->rz / s0; break;
+        case FIN_CG_BETA:
+            sd->beta = s0 / sd->rz;
+            sd->rz = s0;
+            break;
+        case FIN_BI_INIT:
+            sd->rz = s0;
+            sd->beta = 0.0;
+            sd->omega = 1.0;
+            break;
+        case FIN_BI_ALPHA: sd->alpha = sd->rz / s0; break;
+        case FIN_BI_OMEGA: sd->omega = s0 / s1; break;
+        default: {  // the residual of an iteration
+            const double res = sqrt(s0);
+            const int it = sd->it + 1;
+            sd->it = it;
+            sd->res = res;
+            if (it <= sd->maxit) hist[it - 1] = res;
+            if (res < sd->tol && sd->done == 0) sd->done = it;
+            if (mode == FIN_CG_RES_ID) {
+                sd->beta = s0 / sd->rz;
+                sd->rz = s0;
+            } else if (mode == FIN_BI_RES) {
+                sd->beta = (s1 / sd->rz) * (sd->alpha / sd->omega);
+                sd->rz = s1;
+            }
+            mir->res = res;
+            mir->done = sd->done;
+            mir->it = it;
+            break;
+        }
+    }
+}
+
+// Publish this workgroup's partial(s); the last workgroup of the grid runs
+// the finaliser (fin != FIN_NONE: single rank).  The ticket's acq_rel
+// atomic orders every workgroup's partial store before the last one's reads.
+template <int NACC>
+__device__ __forceinline__ void sr_publish(const SrArgs &a, double acc0, double acc1, int bid, int nblk,
+                                           double *sm, int *last) {
+    const double s0 = block_sum(acc0, sm);
+    const double s1 = NACC > 1 ? block_sum(acc1, sm) : 0.0;
+    if (threadIdx.x == 0) {
+        a.part0[bid] = s0;
+        if (NACC > 1) a.part1[bid] = s1;
+    }
+    if (a.fin == FIN_NONE) return;
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(&a.sd->ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        *last = (t == (unsigned)nblk - 1u) ? 1 : 0;
+    }
+    __syncthreads();
+    if (*last == 0) return;
+    __threadfence();
+    sr_fin(a.fin, a.sd, a.part0, a.part1, nblk, a.hist, a.mir, sm);
+    if (threadIdx.x == 0) a.sd->ticket = 0u;
+}
+
+template <int K>
+__device__ __forceinline__ double sr_operand(double v0, double v1, double v2, double al, double be, double om) {
+    if constexpr (K == SRK_CG_P) return v0 + be * v1;
+    else if constexpr (K == SRK_BI_P || K == SRK_BI_PC) return v0 + be * (v1 - om * v2);
+    else if constexpr (K == SRK_BI_S || K == SRK_BI_SC) return v0 - al * v1;
+    else return v0;
+}
+
+template <int K>
+constexpr int sr_nin() {
+    return (K == SRK_BI_P || K == SRK_BI_PC) ? 3 : (K == SRK_CG_P || K == SRK_BI_S || K == SRK_BI_SC) ? 2 : 1;
+}
+
+template <int K>
+constexpr int sr_nacc() {
+    return (K == SRK_BI_S || K == SRK_ST2) ? 2 : (K == SRK_BI_PC || K == SRK_BI_SC) ? 0 : 1;
+}
+
+template <int VEC, int K>
+__global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
+    __shared__ double sm[WAVES];
+    __shared__ int last;
+    if (a.sd->done) return;  // converged: the reference's `if (converged) cycle`
+    constexpr bool CB = (K == SRK_CG_Z || K == SRK_BI_PC || K == SRK_BI_SC);
+    constexpr int NIN = sr_nin<K>();
+    constexpr int NACC = sr_nacc<K>();
+    constexpr bool WU = (K == SRK_CG_P || K == SRK_BI_P || K == SRK_BI_PC || K == SRK_BI_S || K == SRK_BI_SC);
+    constexpr bool WY = (K != SRK_CG_P && K != SRK_CG_X);
+    constexpr bool VD = (K == SRK_BI_P || K == SRK_ST1 || K == SRK_ST2);
+    const double al = a.sd->alpha, be = a.sd->beta, om = a.sd->omega;
+    const double dv = a.cd, ca = a.ca;
+    const int N = a.N;
+    const int lane = threadIdx.x & 63;
+    const i64 i0 = (i64)blockIdx.x * (TPB * VEC) + (i64)VEC * threadIdx.x;
+    const bool act = i0 < N;
+    const int j0 = blockIdx.y * a.JT;
+    const int j1 = min(j0 + a.JT, a.nlines);
+    double acc0 = 0.0, acc1 = 0.0;
+
+    auto in_ptr = [&](int v) -> const double * { return v == 0 ? a.in0 : v == 1 ? a.in1 : a.in2; };
+    // operand line jj: u (and t = u/d for the cbpr2 passes)
+    auto load_line = [&](int jj, double (&u)[VEC], double (&t)[VEC]) {
+        double v[3][VEC];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if (q < NIN) {
+                const double *p = jj < 0 ? a.lo[q] : jj >= a.nlines ? a.hi[q] : in_ptr(q) + (i64)jj * N;
+                ld_vec<VEC>(p != nullptr ? p + i0 : nullptr, act && p != nullptr, v[q]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) v[q][k] = 0.0;
+            }
+        }
+        // a missing line (physical boundary) is zero, whatever the operand formula
+        const bool here = jj < 0 ? a.lo[0] != nullptr : jj >= a.nlines ? a.hi[0] != nullptr : true;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            u[k] = here ? sr_operand<K>(v[0][k], v[1][k], v[2][k], al, be, om) : 0.0;
+            t[k] = CB ? u[k] / dv : u[k];
+        }
+    };
+    auto point_t = [&](i64 e) -> double {  // t at own-slab element e (W/E neighbour of an edge lane)
+        const double v0 = a.in0[e];
+        const double v1 = NIN > 1 ? a.in1[e] : 0.0;
+        const double v2 = NIN > 2 ? a.in2[e] : 0.0;
+        const double u = sr_operand<K>(v0, v1, v2, al, be, om);
+        return CB ? u / dv : u;
+    };
+
+    if (j0 < a.nlines) {
+        double um[VEC], uc[VEC], up[VEC], un[VEC], tm[VEC], tc[VEC], tp[VEC], tn[VEC];
+        load_line(j0 - 1, um, tm);
+        load_line(j0, uc, tc);
+        load_line(j0 + 1, up, tp);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) un[k] = tn[k] = 0.0;
+        for (int j = j0; j < j1; ++j) {
+            if (j + 2 <= j1) load_line(j + 2, un, tn);
+            const i64 row = (i64)j * N;
+            double left = __shfl_up(tc[VEC - 1], 1, 64);
+            double right = __shfl_down(tc[0], 1, 64);
+            if (lane == 0 && act) left = (i0 > 0) ? point_t(row + i0 - 1) : 0.0;
+            if (lane == 63 && act) right = (i0 + VEC < N) ? point_t(row + i0 + VEC) : 0.0;
+            if (i0 == 0) left = 0.0;
+            if (i0 + VEC >= N) right = 0.0;
+            // epilogue operands, issued with the line loads
+            double xv[VEC], rv[VEC], vd[VEC];
+            if (K == SRK_CG_X) {
+                ld_vec<VEC>(a.x + row + i0, act, xv);
+                ld_vec<VEC>(a.r + row + i0, act, rv);
+            }
+            if (VD) ld_vec<VEC>(a.vd + row + i0, act, vd);
+            double yv[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const double W = (k == 0) ? left : tc[k - 1];
+                const double E = (k == VEC - 1) ? right : tc[k + 1];
+                const double s = ((W + E) + tp[k]) + tm[k];
+                const double ax = 4.0 * tc[k] - 1.0 * s;
+                if constexpr (CB) {
+                    yv[k] = tc[k] + ca * (uc[k] - ax);
+                } else {
+                    yv[k] = ax;
+                }
+                if constexpr (K == SRK_CG_X) {
+                    xv[k] = xv[k] + al * uc[k];
+                    rv[k] = rv[k] - al * ax;
+                }
+            }
+            if (act) {
+                if (WU) st_vec<VEC>(a.ou + row + i0, uc);
+                if (WY) st_vec<VEC>(a.oy + row + i0, yv);
+                if (K == SRK_CG_X) {
+                    st_vec<VEC>(a.x + row + i0, xv);
+                    st_vec<VEC>(a.r + row + i0, rv);
+                }
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    if constexpr (K == SRK_CG_P) acc0 = acc0 + yv[k] * uc[k];
+                    else if constexpr (K == SRK_CG_X) acc0 = acc0 + rv[k] * rv[k];
+                    else if constexpr (K == SRK_CG_Z) acc0 = acc0 + uc[k] * yv[k];
+                    else if constexpr (K == SRK_BI_P || K == SRK_ST1) acc0 = acc0 + yv[k] * vd[k];
+                    else if constexpr (K == SRK_BI_S) {
+                        acc0 = acc0 + yv[k] * uc[k];
+                        acc1 = acc1 + yv[k] * yv[k];
+                    } else if constexpr (K == SRK_ST2) {
+                        acc0 = acc0 + yv[k] * vd[k];
+                        acc1 = acc1 + yv[k] * yv[k];
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                um[k] = uc[k];
+                tm[k] = tc[k];
+                uc[k] = up[k];
+                tc[k] = tp[k];
+                up[k] = un[k];
+                tp[k] = tn[k];
+            }
+        }
+    }
+    if constexpr (NACC > 0)
+        sr_publish<NACC>(a, acc0, acc1, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, sm, &last);
+}
+
+// Element-wise passes: grid-stride over double2 chunks, U in flight per thread.
+template <int K, int U>
+__global__ __launch_bounds__(TPB) void k_sr_vec(SrArgs a, i64 n) {
+    __shared__ double sm[WAVES];
+    __shared__ int last;
+    if (a.sd->done) return;
+    constexpr int NACC = K == SRV_BI_X ? 2 : K == SRV_DOT ? 1 : 0;
+    const double al = a.sd->alpha, be = a.sd->beta, om = a.sd->omega;
+    const i64 n2 = n >> 1;
+    const i64 step = (i64)gridDim.x * TPB * U;
+    double acc0 = 0.0, acc1 = 0.0;
+    auto L = [](const double *p, i64 e) { return reinterpret_cast<const double2 *>(p)[e]; };
+    for (i64 b = (i64)blockIdx.x * TPB * U + threadIdx.x; b < n2; b += step) {
+        double2 v0[U], v1[U], v2[U], v3[U], v4[U], v5[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const i64 e = b + (i64)u * TPB;
+            if (e < n2) {
+                if (K == SRV_BI_X) {
+                    v0[u] = L(a.x, e);
+                    v1[u] = L(a.in0, e);  // z1
+                    v2[u] = L(a.in1, e);  // z2
+                    v3[u] = L(a.in2, e);  // s
+                    v4[u] = L(a.e0, e);   // as
+                    v5[u] = L(a.vd, e);   // r0
+                } else if (K == SRV_BI_PE) {
+                    v0[u] = L(a.in0, e);
+                    v1[u] = L(a.in1, e);
+                    v2[u] = L(a.in2, e);
+                } else {
+                    v0[u] = L(a.in0, e);
+                    v1[u] = L(a.in1, e);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const i64 e = b + (i64)u * TPB;
+            if (e >= n2) continue;
+            if constexpr (K == SRV_BI_X) {
+                double2 xn, rn;
+                xn.x = v0[u].x + al * v1[u].x + om * v2[u].x;
+                xn.y = v0[u].y + al * v1[u].y + om * v2[u].y;
+                rn.x = v3[u].x - om * v4[u].x;
+                rn.y = v3[u].y - om * v4[u].y;
+                reinterpret_cast<double2 *>(a.x)[e] = xn;
+                reinterpret_cast<double2 *>(a.r)[e] = rn;
+                acc0 = acc0 + rn.x * rn.x;
+                acc0 = acc0 + rn.y * rn.y;
+                acc1 = acc1 + rn.x * v5[u].x;
+                acc1 = acc1 + rn.y * v5[u].y;
+            } else if constexpr (K == SRV_BI_PE) {
+                double2 o;
+                o.x = v0[u].x + be * (v1[u].x - om * v2[u].x);
+                o.y = v0[u].y + be * (v1[u].y - om * v2[u].y);
+                reinterpret_cast<double2 *>(a.ou)[e] = o;
+            } else if constexpr (K == SRV_BI_SE) {
+                double2 o;
+                o.x = v0[u].x - al * v1[u].x;
+                o.y = v0[u].y - al * v1[u].y;
+                reinterpret_cast<double2 *>(a.ou)[e] = o;
+            } else {
+                acc0 = acc0 + v0[u].x * v1[u].x;
+                acc0 = acc0 + v0[u].y * v1[u].y;
+            }
+        }
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {  // odd-length tail element
+        const i64 e = n - 1;
+        if constexpr (K == SRV_BI_X) {
+            a.x[e] = a.x[e] + al * a.in0[e] + om * a.in1[e];
+            const double rn = a.in2[e] - om * a.e0[e];
+            a.r[e] = rn;
+            acc0 = acc0 + rn * rn;
+            acc1 = acc1 + rn * a.vd[e];
+        } else if constexpr (K == SRV_BI_PE) {
+            a.ou[e] = a.in0[e] + be * (a.in1[e] - om * a.in2[e]);
+        } else if constexpr (K == SRV_BI_SE) {
+            a.ou[e] = a.in0[e] - al * a.in1[e];
+        } else {
+            acc0 = acc0 + a.in0[e] * a.in1[e];
+        }
+    }
+    if constexpr (NACC > 0) sr_publish<NACC>(a, acc0, acc1, blockIdx.x, gridDim.x, sm, &last);
+}
+
+// The finaliser as its own launch (N ranks: after the slab all-reduce; or
+// after a generic preconditioner pass), one workgroup.
+__global__ __launch_bounds__(TPB) void k_sr_fin(int mode, SrDev *sd, const double *p0, const double *p1, int np,
+                                                double *hist, SrMirror *mir) {
+    __shared__ double sm[WAVES];
+    if (sd->done) return;
+    sr_fin(mode, sd, p0, p1, np, hist, mir, sm);
+}
+
+}  // namespace gk

@@ -25,6 +25,7 @@ module gmres_hip_c
     integer(c_int), parameter :: GK_OK = 0
     integer(c_int), parameter :: GK_PREC_IDENTITY = 0, GK_PREC_CBPR2 = 1, GK_PREC_CHEB = 2
     integer(c_int), parameter :: GK_VEC_X = 0, GK_VEC_B = 1
+    integer(c_int), parameter :: GK_SR_PCG = 0, GK_SR_BICGSTAB = 1
     integer(c_int), parameter :: GK_LC_COPY = 0, GK_LC_AXPY = 1, GK_LC_AXPY2 = 2, GK_LC_XPAYMZ = 3, GK_LC_ZERO = 4
     interface
         function gk_last_error() result(p) bind(C, name='gk_last_error')
@@ -168,6 +169,30 @@ module gmres_hip_c
             integer(c_int), value :: form, vout, a, b, c
             real(c_double), value :: s1, s2
         end function
+        integer(c_int) function gk_sr_start(ctx, solver, tol, max_iter) bind(C, name='gk_sr_start')
+            import :: c_int, c_ptr, c_double
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: solver, max_iter
+            real(c_double), value :: tol
+        end function
+        integer(c_int) function gk_sr_iterate(ctx, k) bind(C, name='gk_sr_iterate')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: k
+        end function
+        integer(c_int) function gk_sr_status(ctx, wait, executed, done, res) bind(C, name='gk_sr_status')
+            import :: c_int, c_ptr, c_double
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: wait
+            integer(c_int), intent(out) :: executed, done
+            real(c_double), intent(out) :: res
+        end function
+        integer(c_int) function gk_sr_history(ctx, hist, n) bind(C, name='gk_sr_history')
+            import :: c_int, c_ptr, c_double
+            type(c_ptr), value :: ctx
+            real(c_double), intent(out) :: hist(*)
+            integer(c_int), value :: n
+        end function
         integer(c_size_t) function c_strlen(p) bind(C, name='strlen')
             import :: c_ptr, c_size_t
             type(c_ptr), value :: p
@@ -268,7 +293,9 @@ module gmres_hip
     public :: stencil_vector, precond
     public :: hip_poisson5, hip_identity, hip_cbpr2, hip_chebyshev
     public :: gmres_mgsr_hip, gmres_hh_hip, gmres_hh_prec_hip, hip_release
-    public :: pcg_hip, pbicgstab_hip, pcg_drive, bicgstab_drive
+    public :: pcg_hip, pbicgstab_hip, pcg_drive, bicgstab_drive, pcg_drive_seq, bicgstab_drive_seq
+    !> iterations queued per chunk by the fused short-recurrence drivers
+    integer, public :: hip_sr_chunk = 32
     public :: mgsr_drive, hh_drive, givens_column, back_solve
 
     type(c_ptr) :: opctx = c_null_ptr   ! context of the host-array plug-ins
@@ -471,10 +498,69 @@ contains
         st = gk_get_x(ctx, x)
     end function hh_drive
 
-    !> Preconditioned CG, gmres-free sibling on the same seam: pcg_omp
-    !> (src/cg.f90:154-234) with its scalars on the host and every vector on
-    !> the device.  iter: in = max iterations, out = first i with res < tol.
+    !> The fused short-recurrence solve (gk_sr_*): every scalar stays on the
+    !> device, the iterations are queued in chunks of hip_sr_chunk and chunk k+1
+    !> is queued before the host waits for chunk k; one status read per chunk.
+    !> Iterations after convergence are no-ops on the device (the reference's
+    !> `if (converged) cycle`).  iter: in = max iterations, out = the first i with
+    !> res < tol (unchanged when none), as pcg_omp / pbicgstab_omp return it.
+    integer function sr_drive(ctx, solver, tol, iter, res, want_hist, hist) result(st)
+        type(c_ptr), intent(in) :: ctx
+        integer(c_int), intent(in) :: solver
+        real(8), intent(in) :: tol
+        integer, intent(inout) :: iter
+        real(8), intent(out) :: res
+        logical, intent(in) :: want_hist
+        real(8), intent(inout) :: hist(*)
+        integer(c_int) :: executed, done, k, queued, maxit, wait
+        maxit = int(max(iter, 0), c_int)
+        res = 0.0d0
+        st = gk_sr_start(ctx, solver, tol, maxit); if (st /= GK_OK) return
+        k = int(min(hip_sr_chunk, maxit), c_int)
+        st = gk_sr_iterate(ctx, k); if (st /= GK_OK) return
+        queued = k
+        do
+            if (queued < maxit) then
+                k = int(min(hip_sr_chunk, maxit - queued), c_int)
+                st = gk_sr_iterate(ctx, k); if (st /= GK_OK) return
+                queued = queued + k
+            end if
+            wait = merge(1_c_int, 0_c_int, queued >= maxit)
+            st = gk_sr_status(ctx, wait, executed, done, res); if (st /= GK_OK) return
+            if (done > 0 .or. wait == 1) exit
+        end do
+        st = gk_sr_status(ctx, 1_c_int, executed, done, res); if (st /= GK_OK) return
+        if (done > 0) iter = done
+        if (want_hist .and. executed > 0) st = gk_sr_history(ctx, hist, executed)
+    end function sr_drive
+
+    !> pcg_omp (src/cg.f90:154-234) on the fused device passes.
     integer function pcg_drive(ctx, tol, iter, res, want_hist, hist) result(st)
+        type(c_ptr), intent(in) :: ctx
+        real(8), intent(in) :: tol
+        integer, intent(inout) :: iter
+        real(8), intent(out) :: res
+        logical, intent(in) :: want_hist
+        real(8), intent(inout) :: hist(*)
+        st = sr_drive(ctx, GK_SR_PCG, tol, iter, res, want_hist, hist)
+    end function pcg_drive
+
+    !> pbicgstab_omp (src/bicgstab.f90:91-182) on the fused device passes.
+    integer function bicgstab_drive(ctx, tol, max_iter, res, want_hist, hist) result(st)
+        type(c_ptr), intent(in) :: ctx
+        real(8), intent(in) :: tol
+        integer, intent(inout) :: max_iter
+        real(8), intent(out) :: res
+        logical, intent(in) :: want_hist
+        real(8), intent(inout) :: hist(*)
+        st = sr_drive(ctx, GK_SR_BICGSTAB, tol, max_iter, res, want_hist, hist)
+    end function bicgstab_drive
+
+    !> Preconditioned CG as the reference sequences it: pcg_omp
+    !> (src/cg.f90:154-234) one BLAS-1 operation per device call, its scalars on
+    !> the host (the A/B baseline of the fused pcg_drive, and its cross-check).
+    !> iter: in = max iterations, out = first i with res < tol.
+    integer function pcg_drive_seq(ctx, tol, iter, res, want_hist, hist) result(st)
         type(c_ptr), intent(in) :: ctx
         real(8), intent(in) :: tol
         integer, intent(inout) :: iter
@@ -513,11 +599,12 @@ contains
             end if
             st = gk_vec_lincomb(ctx, GK_LC_AXPY, VP, VZ, VP, VP, beta, 0.0d0); if (st /= GK_OK) return  ! p = z + beta p
         end do
-    end function pcg_drive
+    end function pcg_drive_seq
 
-    !> Preconditioned BiCGSTAB: pbicgstab_omp (src/bicgstab.f90:91-182); the
+    !> Preconditioned BiCGSTAB as the reference sequences it: pbicgstab_omp
+    !> (src/bicgstab.f90:91-182), one operation per device call; the
     !> reference's uninitialised first-iteration accumulators are taken as 0.
-    integer function bicgstab_drive(ctx, tol, max_iter, res, want_hist, hist) result(st)
+    integer function bicgstab_drive_seq(ctx, tol, max_iter, res, want_hist, hist) result(st)
         type(c_ptr), intent(in) :: ctx
         real(8), intent(in) :: tol
         integer, intent(inout) :: max_iter
@@ -563,7 +650,7 @@ contains
             st = gk_vec_lincomb(ctx, GK_LC_XPAYMZ, VP, VR, VP, VAP, beta, omega); if (st /= GK_OK) return
         end do
         max_iter = iters
-    end function bicgstab_drive
+    end function bicgstab_drive_seq
 
     !> Drop-in for pcg_omp (src/cg.f90:154-162).
     subroutine pcg_hip(Ax_op, b, x, tol, iter, res, M_inv, params)
@@ -899,3 +986,26 @@ integer(c_int) function pbicgstab_hip_run(ctx, tol, max_iter, res, want_hist, hi
     pbicgstab_hip_run = bicgstab_drive(ctx, tol, it, res, want_hist /= 0, hist)
     max_iter = it
 end function pbicgstab_hip_run
+
+!> The as-written sequence (one device call per BLAS-1 operation, scalars on
+!> the host): solver 0 = pcg_drive_seq, 1 = bicgstab_drive_seq.
+integer(c_int) function sr_hip_run_seq(ctx, solver, tol, iter, res, want_hist, hist) bind(C, name='sr_hip_run_seq')
+    use, intrinsic :: iso_c_binding
+    use gmres_hip, only: pcg_drive_seq, bicgstab_drive_seq
+    implicit none
+    type(c_ptr), value :: ctx
+    integer(c_int), value :: solver
+    real(c_double), value :: tol
+    integer(c_int), intent(inout) :: iter
+    real(c_double), intent(out) :: res
+    integer(c_int), value :: want_hist
+    real(c_double), intent(inout) :: hist(*)
+    integer :: it
+    it = iter
+    if (solver == 0) then
+        sr_hip_run_seq = pcg_drive_seq(ctx, tol, it, res, want_hist /= 0, hist)
+    else
+        sr_hip_run_seq = bicgstab_drive_seq(ctx, tol, it, res, want_hist /= 0, hist)
+    end if
+    iter = it
+end function sr_hip_run_seq

@@ -400,26 +400,59 @@ def gmres_hh(ctx: Context, tol: float = 1e-15, precondition: bool = False, midcy
     return r
 
 
-def _short(fn_name: str, ctx: Context, tol: float, max_iter: int, want_hist: bool):
+def _short(solver: int, ctx: Context, tol: float, max_iter: int, want_hist: bool, fused: bool):
     if ctx.m < 8:
         raise ValueError("short-recurrence solvers need a context with m >= 8 (scratch vectors)")
     it = ctypes.c_int(max_iter)
     res = ctypes.c_double()
-    hist = np.zeros(max_iter if want_hist else 1)
-    nat.check(getattr(nat.fhost(), fn_name)(ctx.handle, tol, ctypes.byref(it), ctypes.byref(res), int(want_hist),
-                                            _p(hist)), fn_name)
+    hist = np.zeros(max(max_iter, 1) if want_hist else 1)
+    fh = nat.fhost()
+    if fused:
+        name = "pcg_hip_run" if solver == nat.GK_SR_PCG else "pbicgstab_hip_run"
+        st = getattr(fh, name)(ctx.handle, tol, ctypes.byref(it), ctypes.byref(res), int(want_hist), _p(hist))
+    else:
+        name = "sr_hip_run_seq"
+        st = fh.sr_hip_run_seq(ctx.handle, solver, tol, ctypes.byref(it), ctypes.byref(res), int(want_hist),
+                               _p(hist))
+    nat.check(st, name)
     x = ctx.get_x()
     return x, it.value, res.value, (hist[: np.count_nonzero(hist)].copy() if want_hist else None)
 
 
-def pcg(ctx: Context, tol: float = 1e-9, max_iter: int = 1000, want_hist: bool = False):
-    """pcg_omp (src/cg.f90:154-234) on the device: (x, iter, res, hist)."""
-    return _short("pcg_hip_run", ctx, tol, max_iter, want_hist)
+def pcg(ctx: Context, tol: float = 1e-9, max_iter: int = 1000, want_hist: bool = False, fused: bool = True):
+    """pcg_omp (src/cg.f90:154-234) on the device: (x, iter, res, hist).
+    fused = True: the fused passes with the scalars on the device (gk_sr_*);
+    False: the reference's operation sequence, one device call per BLAS-1 op."""
+    return _short(nat.GK_SR_PCG, ctx, tol, max_iter, want_hist, fused)
 
 
-def pbicgstab(ctx: Context, tol: float = 1e-9, max_iter: int = 1000, want_hist: bool = False):
-    """pbicgstab_omp (src/bicgstab.f90:91-182) on the device: (x, iters, res, hist)."""
-    return _short("pbicgstab_hip_run", ctx, tol, max_iter, want_hist)
+def pbicgstab(ctx: Context, tol: float = 1e-9, max_iter: int = 1000, want_hist: bool = False, fused: bool = True):
+    """pbicgstab_omp (src/bicgstab.f90:91-182) on the device: (x, iters, res, hist); fused as in pcg."""
+    return _short(nat.GK_SR_BICGSTAB, ctx, tol, max_iter, want_hist, fused)
+
+
+class SrSolve:
+    """Direct handle on the fused short-recurrence passes (gk_sr_*): start a
+    solve, queue iterations, read the device status -- what bench.py times."""
+
+    def __init__(self, ctx: Context, solver: str, tol: float, max_iter: int):
+        self.ctx = ctx
+        self.solver = {"pcg": nat.GK_SR_PCG, "pbicgstab": nat.GK_SR_BICGSTAB}[solver]
+        nat.check(nat.hip().gk_sr_start(ctx.handle, self.solver, tol, max_iter), "gk_sr_start")
+
+    def iterate(self, k: int) -> None:
+        nat.check(nat.hip().gk_sr_iterate(self.ctx.handle, k), "gk_sr_iterate")
+
+    def status(self, wait_all: bool = True) -> tuple[int, int, float]:
+        ex, dn, res = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+        nat.check(nat.hip().gk_sr_status(self.ctx.handle, int(wait_all), ctypes.byref(ex), ctypes.byref(dn),
+                                         ctypes.byref(res)), "gk_sr_status")
+        return ex.value, dn.value, res.value
+
+    def history(self, n: int) -> np.ndarray:
+        h = np.zeros(max(n, 1))
+        nat.check(nat.hip().gk_sr_history(self.ctx.handle, _p(h), n), "gk_sr_history")
+        return h[:n]
 
 
 # ---------------------------------------------------------------- kernels ---

@@ -56,7 +56,11 @@ extern "C" {
 #define GK_KID_PREC 7    /* temporal-blocked Chebyshev(k) passes (k_cheb_fused) */
 #define GK_KID_HALO 8    /* halo lines with the slab neighbours (RCCL send/recv, local group or device exchange) */
 #define GK_KID_GRAPH 9   /* one launch-path MGS-R step replayed as a hipGraph (its 2j projections, all-reduces, scale) */
-#define GK_NKID 10
+/* short-recurrence passes (gk_sr_*): GK_KID_SR + the pass kind of gk_sr.hpp --
+ * 0 cg_p, 1 cg_x, 2 cg_z, 3 bi_p, 4 bi_pc, 5 bi_s, 6 bi_sc, 7 st1, 8 st2 (line
+ * marches), 9 bi_x, 10 bi_pe, 11 bi_se, 12 dot (element-wise) */
+#define GK_KID_SR 10
+#define GK_NKID 23
 
 typedef struct gk_ctx gk_ctx;
 typedef struct gk_group gk_group;
@@ -234,6 +238,32 @@ int gk_vec_apply(gk_ctx *ctx, int what, int in, int out);
 /* result = <a, b> over all ranks (synchronous). */
 int gk_vec_dot(gk_ctx *ctx, int a, int b, double *result);
 int gk_vec_lincomb(gk_ctx *ctx, int form, int out, int a, int b, int c, double s1, double s2);
+
+/* ------------------------------------- fused short-recurrence solvers ---- */
+/* pcg_omp (src/cg.f90:154-234) and pbicgstab_omp (src/bicgstab.f90:91-182)
+ * with every scalar on the device: one iteration is 2 (PCG, identity) to 5
+ * (BiCGSTAB, cbpr2) fused passes (gmres_amd/csrc/gk_sr.hpp), no host round
+ * trip per dot.  They replace the call sequence the reference's solvers make
+ * through the operator / preconditioner seam (interfaces.f90:13-27): the
+ * Fortran drivers pcg_drive / bicgstab_drive queue iterations in chunks and
+ * read one status per chunk.  Vectors: the context's Krylov columns 0..7
+ * and its w / vj work vectors (needs m >= 7); x stays in HBM (gk_get_x).
+ *
+ * gk_sr_start: x = 0, r = b; PCG: z = M^-1 r, p = z (cg.f90:174-187);
+ *   BiCGSTAB: r0 = p = r (bicgstab.f90:112-118).  max_iter bounds the total
+ *   number of iterations gk_sr_iterate may queue (the history's length).
+ * gk_sr_iterate: queue k more iterations, no host wait.  Iterations after the
+ *   first with res < tol return at entry on the device (`if (converged) cycle`).
+ * gk_sr_status: wait = 0: for the oldest queued chunk; 1: for everything
+ *   queued.  *executed = iterations run, *done = the first iteration with
+ *   res < tol (0: none), *res = residual of the last executed iteration.
+ * gk_sr_history: hist[0..n) = res after iterations 1..n (n <= *executed). */
+#define GK_SR_PCG 0
+#define GK_SR_BICGSTAB 1
+int gk_sr_start(gk_ctx *ctx, int solver, double tol, int max_iter);
+int gk_sr_iterate(gk_ctx *ctx, int k);
+int gk_sr_status(gk_ctx *ctx, int wait, int *executed, int *done, double *res);
+int gk_sr_history(gk_ctx *ctx, double *hist, int n);
 
 /* ---------------------------------------------------------- profiling ---- */
 /* enable = 1: every launch is bracketed by HIP events on the context stream;

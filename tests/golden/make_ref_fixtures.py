@@ -91,6 +91,39 @@ KHIST = [
     ("pbicgstab_omp_cbpr2_256_hist", "pbicgstab_omp", 256, "cbpr2"),
 ]
 
+# round 6: (a) the same truncation histories for 50 iterations at the bench's
+# 4096^2 (the fused device passes' full-size pin), and (b) BiCGSTAB's 256^2
+# identity history at 8 threads beside the 1-thread one above: the spread of the
+# reference against itself (reduction order only) sets the per-iteration band
+# of tests/test_gpu_solver.py's BiCGSTAB history test.
+# (key, solver, N, prec, iterations, threads)
+KHIST_CAP = [
+    ("pcg_omp_identity_4096_hist50", "pcg_omp", 4096, "identity", 50, 1),
+    ("pcg_omp_cbpr2_4096_hist50", "pcg_omp", 4096, "cbpr2", 50, 1),
+    ("pbicgstab_omp_identity_4096_hist50", "pbicgstab_omp", 4096, "identity", 50, 1),
+    ("pbicgstab_omp_cbpr2_4096_hist50", "pbicgstab_omp", 4096, "cbpr2", 50, 1),
+    ("pbicgstab_omp_identity_256_hist_t8", "pbicgstab_omp", 256, "identity", 0, 8),
+    ("pcg_omp_identity_256_hist_t8", "pcg_omp", 256, "identity", 0, 8),
+]
+
+
+def record_khist_cap(key, solver, N, prec, K, threads):
+    """Truncation history of iterations 1..K (K = 0: to convergence) with
+    `threads` OpenMP threads per run (runs in parallel, 8 cores in all)."""
+    t0 = time.time()
+    if K == 0:
+        K = refrun.run(solver, N, 5000, prec, threads=threads).krylov[0]
+    pts = hist_points(K)
+    par = max(1, 8 // threads)
+    with ThreadPoolExecutor(par) as ex:
+        hist = list(ex.map(lambda k: refrun.run(solver, N, k, prec, threads=threads).krylov[1], pts))
+    d = {"solver": solver, "N": N, "prec": prec, "threads": threads, "tol": 1e-9, "hist_iter": pts,
+         "hist_res": hist,
+         "note": "hist_res[i] = the reference's residual after hist_iter[i] iterations (run truncated there)",
+         "wall_s": round(time.time() - t0, 2)}
+    print(f"{key}: {K} history points, {time.time() - t0:.1f} s", flush=True)
+    return key, d
+
 
 def hist_points(K: int) -> list[int]:
     """Iterations of a truncation history: every one."""
@@ -133,7 +166,7 @@ def main() -> None:
     only = None
     if "--only" in sys.argv:
         only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
-        unknown = only - {c[0] for c in SMALL + THREADED + KHIST}
+        unknown = only - {c[0] for c in SMALL + THREADED + KHIST + KHIST_CAP}
         if unknown:
             raise SystemExit(f"unknown cases {sorted(unknown)}")
     refrun.build()
@@ -155,6 +188,11 @@ def main() -> None:
         if (quick and c[2] > 128) or (only is not None and c[0] not in only):
             continue
         key, d = record_khist(*c)
+        out[key] = d
+    for c in KHIST_CAP:
+        if (quick and c[2] > 128) or (only is not None and c[0] not in only):
+            continue
+        key, d = record_khist_cap(*c)
         out[key] = d
     meta = {"_source": "oracle/_ref/ref_driver: the reference's own src/*.f90 (AlexanderGSC/gmres) compiled "
                        "by oracle/Makefile.ref (amdflang 22, -O3 -fopenmp -funroll-loops; interfaces.f90 "
