@@ -82,6 +82,7 @@ _SIGS = {
     "gk_comm_init": (c_int, [c_vp, c_int, c_int, c_int, ctypes.c_char_p]),
     "gk_local_size": (c_int, [c_vp, ctypes.POINTER(c_ll)]),
     "gk_comm_info": (c_int, [c_vp, _ip, _ip]),
+    "gk_peer_info": (c_int, [c_int, c_int, _ip, _ip, _ip]),
     "gk_comm_latency": (c_int, [c_vp, c_int, _dp, _dp]),
     "gk_group_create": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "gk_group_destroy": (c_int, [c_vp]),
@@ -249,6 +250,15 @@ def fhost() -> ctypes.CDLL:
             f.argtypes = args
         _fhost = L
     return _fhost
+
+
+def peer_info(device: int, peer: int) -> dict:
+    """gk_peer_info: peer access and the link between two devices of the node."""
+    a, t, h = c_int(), c_int(), c_int()
+    check(hip().gk_peer_info(int(device), int(peer), ctypes.byref(a), ctypes.byref(t), ctypes.byref(h)),
+          "gk_peer_info")
+    return {"device": int(device), "peer": int(peer), "can_access_peer": bool(a.value),
+            "link_type": {4: "xgmi", 2: "pcie"}.get(t.value, t.value), "hops": h.value}
 
 
 def runtime_info() -> dict:

@@ -137,6 +137,7 @@ struct gk_ctx {
     double *res_gm = nullptr;                       // blocked step: the cycle's Gram table [m+1][RES_SMAX]
     int tune_res_blk = 1;                           // blocked-projection MGS step: S (1 = strict MGS-R)
     int tune_res_pf = 0;                            // strict MGS step on the blocked kernel's LDS prefetch (S = 1)
+    int pend_res_blk = 0, pend_res_pf = -1;         // requested mid-cycle: applied at the next cycle start
     int watchdog_ms = 0;                            // host watchdog of stream waits (0: from the device deadlines)
     bool broken = false;                            // the watchdog fired: a kernel of this context never completed
     unsigned *hold_word = nullptr, *hold_word_dev = nullptr;  // gk_debug_hold_stream's mapped word
@@ -2004,10 +2005,38 @@ int xs_selftest_body(gk_ctx *c, std::string &why) {
 }
 }  // namespace
 
+int gk_peer_info(int device, int peer, int *can_access, int *link_type, int *hops) {
+    if (can_access == nullptr || link_type == nullptr || hops == nullptr) return set_err(GK_ERR_ARG, "null out");
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || peer < 0 || device >= n || peer >= n)
+        return set_err(GK_ERR_ARG, "devices %d, %d outside 0..%d", device, peer, n - 1);
+    *can_access = 1;
+    *link_type = 0;
+    *hops = 0;
+    if (device == peer) return GK_OK;
+    HIPCHK(hipDeviceCanAccessPeer(can_access, device, peer));
+    unsigned lt = 0, hc = 0;
+    HIPCHK(hipExtGetLinkTypeAndHopCount(device, peer, &lt, &hc));
+    *link_type = (int)lt;
+    *hops = (int)hc;
+    return GK_OK;
+}
+
 int gk_xchg_selftest(gk_ctx *c, int timeout_ms) {
     CHK(check_ctx(c));
     if (!c->xs_ready) return set_err(GK_ERR_STATE, "exchange not open");
     HIPCHK(hipSetDevice(c->dev));
+    {  // tests: this rank fails at once without taking part (its peers then miss their deadline)
+        const char *f = std::getenv("GK_DEBUG_SELFTEST_FAIL");
+        if (f != nullptr && f[0] != '\0' && std::atoi(f) == c->rank) {
+            c->xs_on = false;
+            graph_reset(c);
+            if (c->comm == nullptr && c->lg == nullptr) c->comm_ok = c->nranks == 1;
+            return set_err(GK_ERR_COMM, "device exchange self-test failed on rank %d: forced (GK_DEBUG_SELFTEST_FAIL)",
+                           c->rank);
+        }
+    }
     const bool was_on = c->xs_on;
     const int t_keep = c->xs_timeout_ms;
     if (!was_on) graph_reset(c);  // graphs captured on another collective must not replay over this one
@@ -2197,6 +2226,14 @@ int gk_true_residual(gk_ctx *c, double *rel) {
 int gk_mgs_cycle_start(gk_ctx *c, double *beta) {
     CHK(check_ctx(c));
     HIPCHK(hipSetDevice(c->dev));
+    if (c->pend_res_blk != 0 || c->pend_res_pf >= 0) {  // a step change requested mid-cycle (gk_set_tuning)
+        if (c->pend_res_blk != 0) c->tune_res_blk = c->pend_res_blk;
+        if (c->pend_res_pf >= 0) c->tune_res_pf = c->pend_res_pf;
+        c->pend_res_blk = 0;
+        c->pend_res_pf = -1;
+        set_geometry(c);
+        graph_reset(c);
+    }
     CHK(op_precond(c, c->x, c->w, true, gk::ACC_NORM, nullptr, slot(c, 0)));
     CHK(allreduce(c, slot(c, 0), c->last_np));
     CHK(scale(c, c->V, c->w, slot(c, 0), c->last_np, c->hcol));
@@ -2631,12 +2668,23 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_RES_FOLD: c->tune_res_fold = value != 0; break;
         case GK_TUNE_WATCHDOG_MS: c->watchdog_ms = std::max(0, value); break;
         case GK_TUNE_HH_NORM_ORDER: c->tune_hh_norm_order = value != 0; break;
+        // The blocked step reads Gram rows of earlier columns that only a blocked step of the
+        // same cycle wrote: switching the step inside a cycle would use stale rows, so a change
+        // requested while a cycle is open takes effect at the next gk_mgs_cycle_start.
         case GK_TUNE_RES_BLOCK:
             if (value != 1 && value != 2 && value != 4)
                 return set_err(GK_ERR_ARG, "GK_TUNE_RES_BLOCK %d: blocks of 1 (strict MGS-R), 2 or 4 projections", value);
-            c->tune_res_blk = value;
+            if (c->cycle_mgs)
+                c->pend_res_blk = value;
+            else
+                c->tune_res_blk = value;
             break;
-        case GK_TUNE_RES_PF: c->tune_res_pf = value != 0; break;
+        case GK_TUNE_RES_PF:
+            if (c->cycle_mgs)
+                c->pend_res_pf = value != 0;
+            else
+                c->tune_res_pf = value != 0;
+            break;
         case GK_TUNE_RES_LOOKAHEAD:  // (round 5: measured slower than the plain blocked step, removed)
             if (value != 0)
                 return set_err(GK_ERR_ARG, "GK_TUNE_RES_LOOKAHEAD was removed (look-ahead blocked step measured slower: "

@@ -14,7 +14,14 @@ Rendezvous: rank 0 listens on an ephemeral 127.0.0.1 port and publishes
 the launcher's pid, which torch.distributed.run's ranks share); the other
 ranks poll for that file, skip it while the pid it names is not alive (a file
 left by a crashed launch), connect and present the token, which rank 0 checks
-before it counts the rank.  Every collective is a gather to rank 0 followed by
+before it counts the rank.
+
+Authentication comes before any deserialisation: the hello is raw
+bytes -- the 32-character token and the rank as a 4-byte integer -- compared
+with hmac.compare_digest, and rank 0 answers with raw bytes too; only links
+that passed it ever carry pickles.  The rendezvous file is created mode 0600,
+and a joining rank uses it only if this user owns it, so neither the token nor
+the port can be read or planted by another local user.  Every collective is a gather to rank 0 followed by
 a broadcast of the result, in rank order, so all ranks see identical values.
 
 Every wait is bounded (round 5): the connect,
@@ -24,6 +31,7 @@ that never answered, so a live-but-stuck peer cannot block the others forever.
 """
 from __future__ import annotations
 
+import hmac
 import os
 import pickle
 import secrets
@@ -33,6 +41,8 @@ import tempfile
 import time
 
 _HDR = struct.Struct("!Q")
+_HELLO = struct.Struct("!32sI")  # token (32 hex characters), rank
+_ACK = b"OK"
 
 
 def launch_key() -> str:
@@ -83,6 +93,12 @@ class _Link:
         (n,) = _HDR.unpack(self._exact(_HDR.size, timeout))
         return pickle.loads(self._exact(n, timeout))
 
+    def send_raw(self, data: bytes) -> None:
+        self.sock.sendall(data)
+
+    def recv_raw(self, n: int, timeout: float) -> bytes:
+        return self._exact(n, timeout)
+
     def close(self) -> None:
         try:
             self.sock.close()
@@ -116,7 +132,8 @@ class Ctl:
         ls.listen(self.world)
         self._listener = ls
         tmp = self._file + f".{os.getpid()}.tmp"
-        with open(tmp, "w") as f:
+        fd = os.open(tmp, os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o600)  # owner-only: the token is a secret
+        with os.fdopen(fd, "w") as f:
             f.write(f"{ls.getsockname()[1]} {token} {os.getpid()}\n")
         os.replace(tmp, self._file)  # atomic: a reader sees all of it or nothing
         got: dict[int, _Link] = {}
@@ -131,32 +148,34 @@ class Ctl:
             except socket.timeout:
                 continue
             link = _Link(s, "a connecting rank")
-            try:
-                hello = link.recv(min(10.0, max(left, 0.1)))
-            except (TimeoutError, ConnectionError, pickle.UnpicklingError, EOFError):
+            try:  # raw bytes: nothing is unpickled before the token matched
+                tok, r = _HELLO.unpack(link.recv_raw(_HELLO.size, min(10.0, max(left, 0.1))))
+            except (TimeoutError, ConnectionError, struct.error):
                 link.close()  # not one of ours (or too slow to say hello): drop it
                 continue
-            if not (isinstance(hello, tuple) and len(hello) == 2 and hello[0] == token
-                    and isinstance(hello[1], int) and 0 < hello[1] < self.world and hello[1] not in got):
+            if not (hmac.compare_digest(tok, token.encode()) and 0 < r < self.world and r not in got):
                 link.close()
                 continue
-            link.who = f"rank {hello[1]}"
-            link.send("ok")
-            got[hello[1]] = link
+            link.who = f"rank {r}"
+            link.send_raw(_ACK)
+            got[r] = link
         self._peers = [got[r] for r in range(1, self.world)]
 
     def _join(self, deadline: float) -> None:
         last = None
         while True:
             try:
+                st = os.stat(self._file)
+                if st.st_uid != os.getuid() or (st.st_mode & 0o077):
+                    raise ValueError(f"rendezvous file {self._file} is not this user's private file")
                 port, token, pid = open(self._file).read().split()
                 if not _pid_alive(int(pid)):
                     raise ValueError(f"rendezvous file of a dead rank 0 (pid {pid})")
                 left = max(0.1, deadline - time.monotonic())
                 s = socket.create_connection(("127.0.0.1", int(port)), timeout=min(5.0, left))
                 link = _Link(s, "rank 0")
-                link.send((token, self.rank))
-                if link.recv(min(10.0, left)) != "ok":
+                link.send_raw(_HELLO.pack(token.encode(), self.rank))
+                if link.recv_raw(len(_ACK), min(10.0, left)) != _ACK:
                     link.close()
                     raise ConnectionError("rank 0 refused the hello")
                 self._conn = link

@@ -113,7 +113,10 @@ int gk_comm_init_local(gk_ctx *ctx, gk_group *g, int rank, int max_lines);
  *   gk_xchg_selftest    collective check of the reduction and halo paths with
  *                       a deadline; GK_ERR_COMM if any granule is missing or
  *                       wrong.  Also usable after gk_comm_init (RCCL present):
- *                       a failed test leaves the exchange disabled.
+ *                       a failed test leaves the exchange disabled.  (Tests:
+ *                       env GK_DEBUG_SELFTEST_FAIL=<rank> makes that rank fail
+ *                       at once without taking part; its peers then miss
+ *                       their deadline.)
  * Usable together with gk_comm_init (then RCCL remains the fallback).
  * A missed deadline during a solve (GK_ERR_COMM, naming the late rank or
  * workgroup) retires the exchange of that context: its later exchanges fail at
@@ -136,6 +139,12 @@ int gk_local_size(gk_ctx *ctx, long long *nloc);
 #define GK_COMM_LOCAL 2
 #define GK_COMM_XGMI 3
 int gk_comm_info(gk_ctx *ctx, int *kind, int *nranks_seen);
+/* First contact between two devices of the node (no context needed): whether
+ * `device` can map `peer`'s memory (hipDeviceCanAccessPeer) and the link type
+ * and hop count between them (hipExtGetLinkTypeAndHopCount; link_type as HIP's
+ * HSA_AMD_LINK_INFO_TYPE: 4 = xGMI, 2 = PCIe).  bench.py logs it for every rank
+ * pair of an N-GPU line.  device == peer: can_access 1, hops 0. */
+int gk_peer_info(int device, int peer, int *can_access, int *link_type, int *hops);
 /* Collective, every rank together: the mean cost (us, HIP events on the
  * context stream) of one all-reduce of a projection's partial slab and of one
  * halo exchange (one grid line with each neighbour) through the collective in

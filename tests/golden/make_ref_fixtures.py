@@ -102,7 +102,12 @@ KHIST_CAP = [
     ("pcg_omp_cbpr2_4096_hist50", "pcg_omp", 4096, "cbpr2", 50, 1),
     ("pbicgstab_omp_identity_4096_hist50", "pbicgstab_omp", 4096, "identity", 50, 1),
     ("pbicgstab_omp_cbpr2_4096_hist50", "pbicgstab_omp", 4096, "cbpr2", 50, 1),
+    ("pbicgstab_omp_identity_4096_hist50_t8", "pbicgstab_omp", 4096, "identity", 50, 8),
+    ("pbicgstab_omp_cbpr2_4096_hist50_t8", "pbicgstab_omp", 4096, "cbpr2", 50, 8),
     ("pbicgstab_omp_identity_256_hist_t8", "pbicgstab_omp", 256, "identity", 0, 8),
+    ("pbicgstab_omp_cbpr2_256_hist_t8", "pbicgstab_omp", 256, "cbpr2", 0, 8),
+    ("pbicgstab_omp_identity_128_hist_t8", "pbicgstab_omp", 128, "identity", 0, 8),
+    ("pbicgstab_omp_cbpr2_128_hist_t8", "pbicgstab_omp", 128, "cbpr2", 0, 8),
     ("pcg_omp_identity_256_hist_t8", "pcg_omp", 256, "identity", 0, 8),
 ]
 

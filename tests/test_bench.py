@@ -316,6 +316,61 @@ def test_control_plane_bounds_a_stuck_peer(tmp_path):
     assert "rank 1" in msg and dt < 6, (msg, dt)
 
 
+class _Planted:
+    """A pickle that creates a file when unpickled (a stranger's hello)."""
+
+    def __init__(self, path):
+        self.path = path
+
+    def __reduce__(self):
+        return (open, (self.path, "w"))
+
+
+def test_control_plane_authenticates_before_unpickling(tmp_path):
+    """rank 0 reads a connecting peer's hello as raw bytes and
+    checks the token before anything is unpickled -- a stranger's pickled payload
+    is dropped unread -- and the rendezvous file (port + token) is private."""
+    import pickle
+    import socket
+    import stat
+    import struct
+    import threading
+
+    from gmres_amd.ctl import Ctl
+
+    marker = tmp_path / "unpickled"
+    out = {}
+
+    def rank0():
+        c = Ctl(0, 2, key="auth", timeout=30, rdzv_dir=str(tmp_path))
+        out["v"] = c.allgather("r0")
+        c.close()
+
+    t = threading.Thread(target=rank0)
+    t.start()
+    f = tmp_path / "gk_ctl_auth"
+    for _ in range(600):
+        if f.exists():
+            break
+        time.sleep(0.01)
+    assert stat.S_IMODE(f.stat().st_mode) == 0o600
+    port = int(f.read_text().split()[0])
+    data = pickle.dumps(_Planted(str(marker)))
+    with socket.create_connection(("127.0.0.1", port)) as s:
+        s.sendall(struct.pack("!Q", len(data)) + data)
+        s.settimeout(5)
+        try:
+            assert s.recv(16) == b""  # dropped: closed without an answer
+        except (ConnectionResetError, socket.timeout):
+            pass
+    c1 = Ctl(1, 2, key="auth", timeout=30, rdzv_dir=str(tmp_path))
+    v = c1.allgather("r1")
+    c1.close()
+    t.join(timeout=30)
+    assert v == out["v"] == ["r0", "r1"]
+    assert not marker.exists()
+
+
 def test_control_plane_skips_a_stale_rendezvous_file(tmp_path):
     """A rendezvous file left by a crashed launch (its rank 0 dead) is not
     connected to: the joining rank waits for the live rank 0's file."""

@@ -31,9 +31,14 @@ REF = json.load(open(os.path.join(HERE, "golden", "reference_runs.json")))
 
 
 def _tune(c, S, share=1):
+    """S = 2 / 4: the blocked step; S = 0: the strict step on the prefetching
+    blocked kernel (GK_TUNE_RES_PF)."""
     from gmres_amd import _native as nat
 
-    c.tune(nat.GK_TUNE_RES_BLOCK, S)
+    if S == 0:
+        c.tune(nat.GK_TUNE_RES_PF, 1)
+    else:
+        c.tune(nat.GK_TUNE_RES_BLOCK, S)
     if share > 1:
         c.tune(nat.GK_TUNE_RES, 1)
         c.tune(nat.GK_TUNE_RES_SHARE, share)
@@ -147,14 +152,16 @@ def test_blocked_ragged_slabs_vs_oracle(oracle, S, N, m):
     _contract(r.hist_res, ref.hist_res)
 
 
-@pytest.mark.parametrize("S", [2, 4])
+@pytest.mark.parametrize("S", [2, 4, 0])
 @pytest.mark.parametrize("N,R", [(1448, 2), (2048, 4)])
 def test_blocked_row_block_ranks(S, N, R):
     """R row-block ranks on one GPU through the device exchange, 256 / R
     workgroups each: the blocked step's multi-value all-gather and rank-total hop
     (value slot v of each replica) -- one cycle against a single-context blocked
     run (1e-9; only the dot summation order differs) and every rank taking the
-    same decisions."""
+    same decisions.  S = 0: the strict step on the prefetching kernel
+    (GK_TUNE_RES_PF), whose split prefetch (BLK_PF_SPLIT: the non-polling waves
+    prefetch so the rank-total pusher is not delayed) exists for this N-rank case."""
     import gmres_amd as ga
 
     single, _, _ = _run(N, 95, S, 1)
@@ -169,7 +176,7 @@ def test_blocked_row_block_ranks(S, N, R):
             c.xchg_local()
             _tune(c, S, share=R)
         plans = [c.res_info() for c in ctxs]
-        assert all(p["variant"] == "blocked" and p["blk"] == S and p["G"] == 256 // R for p in plans), plans
+        assert all(p["variant"] == "blocked" and p["blk"] == max(S, 1) and p["G"] == 256 // R for p in plans), plans
 
         def work(q):
             try:
@@ -199,6 +206,31 @@ def test_blocked_row_block_ranks(S, N, R):
         assert prof["res"][1] >= 95 and prof["proj"][1] <= 1, prof
     assert res[0].hist_res[0] == pytest.approx(single.hist_res[0], rel=1e-9)
     assert np.allclose(res[0].final_err[:95], single.final_err[:95], rtol=1e-6, atol=0)
+
+
+def test_step_change_inside_a_cycle_waits_for_the_next_cycle():
+    """the blocked step reads Gram rows only a blocked step of the same
+    cycle wrote, so GK_TUNE_RES_BLOCK / GK_TUNE_RES_PF set while a cycle is open
+    apply from the next gk_mgs_cycle_start: the next solve equals a fresh blocked
+    solve bit for bit."""
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+
+    with ga.Context(1024, 95) as c:
+        c.set_rhs_ones()
+        ga.gmres_mgsr(c, 1e-15, max_cycles=1, want_verr=False)  # leaves a cycle open
+        c.tune(nat.GK_TUNE_RES_BLOCK, 2)
+        assert c.res_info()["blk"] == 1  # pending
+        r2 = ga.gmres_mgsr(c, 1e-15, max_cycles=2, want_verr=False, want_hist=True)
+        assert c.res_info()["blk"] == 2
+        c.tune(nat.GK_TUNE_RES_BLOCK, 1)
+        c.tune(nat.GK_TUNE_RES_PF, 1)
+        assert c.res_info()["blk"] == 2
+        ga.gmres_mgsr(c, 1e-15, max_cycles=1, want_verr=False)
+        assert c.res_info()["blk"] == 1 and c.res_info()["variant"] == "blocked"
+    fresh, _, _ = _run(1024, 95, 2, 2)
+    assert np.array_equal(r2.hist_res, fresh.hist_res)
+    assert np.array_equal(r2.final_err, fresh.final_err)
 
 
 def test_blocked_knob_rejects_other_sizes():
@@ -247,8 +279,9 @@ def test_strict_prefetch_build_vs_reference(share, chunks):
 
 
 def test_strict_prefetch_build_ranks_and_ragged(oracle):
-    """Ragged slabs against the oracle (1e-9 over ten cycles) and 2 row-block ranks at
-    1448^2 (the 4096^2 / 8 load) against the reference's own cycle."""
+    """Ragged slabs against the oracle (1e-9 over ten cycles) and the 1448^2 grid
+    (the 4096^2 / 8 load, single context) against the reference's own cycle; the
+    row-block ranks of this step are test_blocked_row_block_ranks[S=0]."""
     from gmres_amd import _native as nat
     import gmres_amd as ga
 

@@ -387,3 +387,73 @@ def test_bench_two_ranks_default_collective_on_one_gpu():
     assert line["config"]["collective"] == "xgmi-device-exchange"
     assert line["config"]["comm_ranks_seen"] == 2
     assert line["check"]["pass"], line["check"]
+
+
+# ------------------------------------- a self-test that fails on one rank ----
+
+def _failing_selftest_worker(rank, port, hq, hin, outq):
+    import os
+    import sys
+    import time
+
+    try:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        import gmres_amd as ga
+        from gmres_amd.ctl import Ctl
+
+        N, m = 64, 16
+        l0, nl = ga.slab_partition(N, 2)[rank]
+        c = ga.Context(N, m, device=0, line0=l0, nlines=nl)
+        c.comm_init_xgmi(2, rank, N // 2)
+        ctl = Ctl(rank, 2, key=f"selftest_fail_{port}", timeout=120)
+        t0 = time.perf_counter()
+        out = bench.setup_xgmi(c, ctl, rank, required=False)
+        dt = time.perf_counter() - t0
+        rec = bench.first_contact_record(c, ctl, rank, 2, 0)
+        outq.put((rank, "ok", (out, dt, getattr(c, "xchg_error", ""), rec)))
+        ctl.barrier()
+        ctl.close()
+        c.close()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        outq.put((rank, "error", repr(e)))
+
+
+def test_selftest_failure_on_one_rank_is_agreed_within_the_deadline():
+    """two processes on one GPU, the real device exchange
+    over IPC, rank 1's self-test forced to fail (GK_DEBUG_SELFTEST_FAIL=1: it
+    takes no part).  Rank 0 misses its 5 s deadline waiting for rank 1's
+    granules; both ranks then take bench.setup_xgmi's documented decision
+    together (exchange off on every rank; the caller falls back to RCCL or
+    fails), each within the deadline plus margin, and the first-contact record
+    names both errors."""
+    import os
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ["GK_DEBUG_SELFTEST_FAIL"] = "1"  # inherited by the spawned ranks
+    try:
+        ctx = mp.get_context("spawn")
+        hq, outq = ctx.Queue(), ctx.Queue()
+        ps = [ctx.Process(target=_failing_selftest_worker, args=(r, port, hq, None, outq)) for r in range(2)]
+        for p in ps:
+            p.start()
+        try:
+            got = dict((r, (kind, val)) for r, kind, val in (outq.get(timeout=120) for _ in range(2)))
+        finally:
+            for p in ps:
+                p.join(timeout=60)
+                if p.is_alive():
+                    p.kill()
+    finally:
+        os.environ.pop("GK_DEBUG_SELFTEST_FAIL", None)
+    assert [p.exitcode for p in ps] == [0, 0]
+    for r in range(2):
+        assert got[r][0] == "ok", got[r]
+    (o0, dt0, e0, rec0), (o1, dt1, e1, rec1) = got[0][1], got[1][1]
+    assert o0 is None and o1 is None  # the same decision on every rank: no device exchange
+    assert "forced" in e1 and "rank 0" in e0 and ("deadline" in e0 or "rank 1" in e0), (e0, e1)
+    assert dt1 < 5.0 + 3.0 and dt0 < 5.0 + 3.0, (dt0, dt1)  # the agreement waits one deadline, not forever
+    assert rec0["selftest_errors"][1] and rec0["same_device_rehearsal"]
