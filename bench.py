@@ -852,7 +852,8 @@ def sr_cpu_baseline(solver: str, N: int, prec: str, k1: int = 4, k2: int = 0, bu
                                                                                        "omp_threads")}}
 
 
-def sr_legs(ga, iters: int = 400, with_cpu: bool = True) -> list[dict]:
+def sr_legs(ga, iters: int = 400, with_cpu: bool = True, tune: list[str] | None = None,
+            legs: list[tuple[str, str]] | None = None) -> list[dict]:
     """SURVEY 8f rank 3 at the bench's 4096^2: pcg_omp / pbicgstab_omp on the fused
     device passes (gk_sr_*).  Per leg, on a fresh context: the first 50 iterations
     from x0 = 0 against the reference's own truncated run (tests/golden
@@ -866,11 +867,14 @@ def sr_legs(ga, iters: int = 400, with_cpu: bool = True) -> list[dict]:
     N = 4096
     n = N * N
     runs = json.load(open(os.path.join(GOLDEN_DIR, "reference_runs.json")))
-    for solver, prec in SR_LEGS:
+    for solver, prec in legs or SR_LEGS:
         leg = {"baseline_config": None, "kind": "short-recurrence solver (SURVEY 8f rank 3)",
                "workload": f"{N}x{N} Poisson-2D fp64, {solver}_omp ({'no precond' if prec == 'identity' else prec}), "
                            f"fused device passes", "solver": solver, "precond": prec}
         with ga.Context(N, 8) as c:
+            for kv in tune or []:
+                k, v = kv.split("=")
+                c.tune(int(k), int(v))
             c.set_precond(prec, (8.2, 0.2), 1)
             c.set_rhs_ones()
             g = runs.get(f"{solver}_omp_{prec}_{N}_hist50")
@@ -884,6 +888,14 @@ def sr_legs(ga, iters: int = 400, with_cpu: bool = True) -> list[dict]:
                 leg["check"] = {"golden_source": f"tests/golden/reference_runs.json:{solver}_omp_{prec}_{N}_hist50",
                                 "iterations_compared": int(len(h)), "max_rel_dev": float(dev.max()), "tol": 1e-9,
                                 "pass": bool(dev.max() <= 1e-9)}
+                g8 = runs.get(f"{solver}_omp_{prec}_{N}_hist50_t8")
+                if solver == "pbicgstab" and g8:  # chaotic recurrence: the reference's own spread sets the band
+                    from tests.sr_band import BAND_F, bicgstab_band
+
+                    ok, worst = bicgstab_band(h, g["hist_res"], g8["hist_res"])
+                    leg["check"].update({"tol": f"band: |ln(h/r)| <= ln(1 + {BAND_F:g} S_k), S_k = the reference's own "
+                                                "1-vs-8-thread spread (tests/sr_band.py)",
+                                         "band_worst": round(worst, 4), "pass": ok})
             s = ga.SrSolve(c, solver, 0.0, iters)  # timed: graphs, no events
             c.sync()
             t0 = time.perf_counter()
@@ -1005,7 +1017,8 @@ def main() -> None:
     if args.sr_only:
         import gmres_amd as ga
 
-        print(json.dumps({"sr_legs": sr_legs(ga, with_cpu=not args.no_cpu)}), flush=True)
+        print(json.dumps({"sr_legs": sr_legs(ga, with_cpu=not args.no_cpu, tune=args.tune), "tune": args.tune}),
+              flush=True)
         return
     maybe_self_launch(args, sys.argv[1:])
 

@@ -24,6 +24,8 @@ HEADER = os.path.join(os.path.dirname(PKG), "include", "gmres_hip.h")
 GK_OK = 0
 GK_ERR_COMM = -6
 GK_TUNE_PROJ_NT = 0
+GK_TUNE_STENCIL_BLOCKS = 2
+GK_TUNE_SR_BLOCKS = 28
 GK_TUNE_XCHG_TIMEOUT_MS = 7
 GK_TUNE_RES, GK_TUNE_RES_R2, GK_TUNE_RES_SHARE, GK_TUNE_RES_TIMEOUT_MS = 8, 9, 10, 11
 GK_TUNE_VERR_ORDER = 14

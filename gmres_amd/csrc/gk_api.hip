@@ -96,6 +96,7 @@ struct gk_ctx {
     double *w = nullptr, *z = nullptr, *aux = nullptr, *dA = nullptr, *dB = nullptr;
     double *x = nullptr, *b = nullptr, *vj = nullptr, *hlo = nullptr, *hhi = nullptr;
     double *dh = nullptr;  // deep halos of the Chebyshev pass inputs: [3 vectors][lo, hi][CF_HMAX lines][N]
+    double *zline = nullptr;  // N zeros (the short-recurrence marches' line past a physical boundary)
     double *red = nullptr;   // NSLOT * NPMAX partial slabs
     double *hcol = nullptr;  // m+2 Hessenberg column / scalars
     double *ydev = nullptr;  // m+1
@@ -162,6 +163,9 @@ struct gk_ctx {
     // launch geometry
     int vec = 2, JT = 16;
     dim3 sgrid;
+    int sr_JT = 64, tune_sr_blocks = 0;  // the short-recurrence marches' geometry (gk_sr_*)
+    dim3 sr_sgrid;
+    int np_sr = 0;
     int np_st = 0, np_pj = 0, nblk_stream = 0;
     int last_np = 0;          // partial count written by the last ACC-carrying sweep
     int tune_cheb_fused = 1;  // temporal-blocked Chebyshev sweeps (single slab)
@@ -582,6 +586,19 @@ void set_geometry(gk_ctx *c) {
     c->JT = JT;
     c->sgrid = dim3(gx, gy, 1);
     c->np_st = gx * gy;
+    {  // the short-recurrence marches: fewer, longer marches (each re-reads 2 neighbour lines per march)
+        const int srt = c->tune_sr_blocks > 0 ? c->tune_sr_blocks : 512;
+        int sjt = (int)std::max<i64>(1, ((i64)ml * gx + srt - 1) / srt);
+        if (sjt > 256) sjt = 256;
+        int sgy = (ml + sjt - 1) / sjt;
+        while ((i64)gx * sgy > gk::NPMAX) {
+            ++sjt;
+            sgy = (ml + sjt - 1) / sjt;
+        }
+        c->sr_JT = sjt;
+        c->sr_sgrid = dim3(gx, sgy, 1);
+        c->np_sr = gx * sgy;
+    }
     // projection kernels: fixed workgroup count derived from the largest slab
     const i64 nmax2 = ((i64)ml * N + 1) / 2;
     i64 npj = (nmax2 + (i64)gk::TPB * gk::UNR - 1) / ((i64)gk::TPB * gk::UNR);
@@ -1672,6 +1689,8 @@ int gk_create(int device, int nside, int line0, int nlines, int m, gk_ctx **out)
     if (hipMalloc(&c->hlo, sizeof(double) * nside) != hipSuccess ||
         hipMalloc(&c->hhi, sizeof(double) * nside) != hipSuccess ||
         hipMalloc(&c->dh, sizeof(double) * 6 * gk::CF_HMAX * (size_t)nside) != hipSuccess ||
+        hipMalloc(&c->zline, sizeof(double) * (size_t)nside) != hipSuccess ||
+        hipMemsetAsync(c->zline, 0, sizeof(double) * (size_t)nside, c->st) != hipSuccess ||
         hipMalloc(&c->red, sizeof(double) * NSLOT * gk::NPMAX) != hipSuccess ||
         hipMalloc(&c->hcol, sizeof(double) * (m + 2)) != hipSuccess ||
         hipMalloc(&c->ydev, sizeof(double) * (m + 1)) != hipSuccess ||
@@ -1748,7 +1767,7 @@ int gk_destroy(gk_ctx *c) {
     if (c->sr_hist) (void)hipFree(c->sr_hist);
     for (hipEvent_t e : c->sr_pend) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->sr_evfree) (void)hipEventDestroy(e);
-    double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi, c->dh,
+    double *bufs[] = {c->V, c->w, c->z, c->aux, c->dA, c->dB, c->x, c->b, c->vj, c->hlo, c->hhi, c->dh, c->zline,
                       c->red, c->hcol, c->ydev, c->hb, c->scal, c->Vb, c->gram_slab, c->gram_out};
     for (double *p : bufs)
         if (p) (void)hipFree(p);
@@ -2679,6 +2698,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
             else
                 c->tune_res_blk = value;
             break;
+        case GK_TUNE_SR_BLOCKS: c->tune_sr_blocks = std::max(0, value); break;
         case GK_TUNE_RES_PF:
             if (c->cycle_mgs)
                 c->pend_res_pf = value != 0;
@@ -3206,9 +3226,10 @@ gk::SrArgs sr_args(gk_ctx *c) {
     a.mir = c->sr_mir_dev;
     a.part0 = slot(c, 0);
     a.part1 = slot(c, 1);
+    a.zl = c->zline;
     a.N = c->N;
     a.nlines = c->nlines;
-    a.JT = c->JT;
+    a.JT = c->sr_JT;
     // cbpr2 coefficients exactly as chebyshev.f90:19-25 (precond_sweeps)
     const double cc = (c->p1 - c->p0) / 2.0, d = (c->p1 + c->p0) / 2.0;
     double al = 1.0 / d;
@@ -3251,12 +3272,12 @@ int sr_march(gk_ctx *c, gk::SrArgs a, int fin) {
     {
         ProfScope ps(c, GK_KID_SR + K);
         if (c->vec == 2)
-            gk::k_sr_march<2, K><<<c->sgrid, gk::TPB, 0, c->st>>>(a);
+            gk::k_sr_march<2, K><<<c->sr_sgrid, gk::TPB, 0, c->st>>>(a);
         else
-            gk::k_sr_march<1, K><<<c->sgrid, gk::TPB, 0, c->st>>>(a);
+            gk::k_sr_march<1, K><<<c->sr_sgrid, gk::TPB, 0, c->st>>>(a);
         LAUNCHCHK();
     }
-    if (slabs) CHK(sr_fin_after(c, fin, c->np_st, gk::sr_nacc<K>() > 1));
+    if (slabs) CHK(sr_fin_after(c, fin, c->np_sr, gk::sr_nacc<K>() > 1));
     return GK_OK;
 }
 

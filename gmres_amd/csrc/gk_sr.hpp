@@ -89,6 +89,7 @@ enum {
 struct SrArgs {
     const double *in0, *in1, *in2;  // operand inputs (k_sr_march) / element-wise inputs (k_sr_vec)
     const double *lo[3], *hi[3];    // halo line of each operand input (nullptr: physical boundary)
+    const double *zl;               // N zeros: the line beyond a physical boundary
     double *ou;                     // the operand u itself (p, s)
     double *oy;                     // the stencil output (ap, as, z, z1, z2)
     double *x, *r;                  // updated in place (CG_X; BI_X)
@@ -102,12 +103,32 @@ struct SrArgs {
     int N, nlines, JT, fin;
 };
 
+// Partials cross workgroups (and XCDs, whose L2s are not coherent) inside one
+// launch: written and read as agent-scope relaxed atomics, which go to the
+// coherence point, so no L2 write-back fence is needed.  (A release on the
+// ticket writes back the XCD's whole L2: with acq_rel tickets the dot-carrying
+// passes ran at 0.26-0.33 of HBM, measured r06c.)
+__device__ __forceinline__ void sr_put(double *p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double sr_get(const double *p) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// Fixed-order sum of a slab written by sr_put (k_sr_fin: any partial slab).
+__device__ __forceinline__ double sr_slab_sum(const double *p, int np, double *sm) {
+    double s = 0.0;
+    for (int k = threadIdx.x; k < np; k += TPB) s += sr_get(p + k);
+    return block_sum(s, sm);
+}
+
 // The finaliser: one workgroup (all TPB threads) after every partial of the
 // pass is visible.
 __device__ __forceinline__ void sr_fin(int mode, SrDev *sd, const double *p0, const double *p1, int np,
                                        double *hist, SrMirror *mir, double *sm) {
-    const double s0 = reduce_slab(p0, np, sm);
-    const double s1 = (mode == FIN_BI_OMEGA || mode == FIN_BI_RES) ? reduce_slab(p1, np, sm) : 0.0;
+    const double s0 = sr_slab_sum(p0, np, sm);
+    const double s1 = (mode == FIN_BI_OMEGA || mode == FIN_BI_RES) ? sr_slab_sum(p1, np, sm) : 0.0;
     if (threadIdx.x != 0) return;
     switch (mode) {
         case FIN_CG_INIT:
@@ -149,25 +170,27 @@ __device__ __forceinline__ void sr_fin(int mode, SrDev *sd, const double *p0, co
 }
 
 // Publish this workgroup's partial(s); the last workgroup of the grid runs
-// the finaliser (fin != FIN_NONE: single rank).  The ticket's acq_rel
-// atomic orders every workgroup's partial store before the last one's reads.
+// the finaliser (fin != FIN_NONE: single rank).  Each partial is stored at the
+// coherence point (sr_put) and acknowledged (vmcnt(0)) before the workgroup
+// takes its ticket, so the workgroup that takes the last ticket finds every
+// partial there (sr_get).
 template <int NACC>
 __device__ __forceinline__ void sr_publish(const SrArgs &a, double acc0, double acc1, int bid, int nblk,
                                            double *sm, int *last) {
     const double s0 = block_sum(acc0, sm);
     const double s1 = NACC > 1 ? block_sum(acc1, sm) : 0.0;
     if (threadIdx.x == 0) {
-        a.part0[bid] = s0;
-        if (NACC > 1) a.part1[bid] = s1;
+        sr_put(a.part0 + bid, s0);
+        if (NACC > 1) sr_put(a.part1 + bid, s1);
     }
     if (a.fin == FIN_NONE) return;
     if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add(&a.sd->ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial stores are acknowledged
+        const unsigned t = __hip_atomic_fetch_add(&a.sd->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *last = (t == (unsigned)nblk - 1u) ? 1 : 0;
     }
     __syncthreads();
     if (*last == 0) return;
-    __threadfence();
     sr_fin(a.fin, a.sd, a.part0, a.part1, nblk, a.hist, a.mir, sm);
     if (threadIdx.x == 0) a.sd->ticket = 0u;
 }
@@ -189,6 +212,13 @@ template <int K>
 constexpr int sr_nacc() {
     return (K == SRK_BI_S || K == SRK_ST2) ? 2 : (K == SRK_BI_PC || K == SRK_BI_SC) ? 0 : 1;
 }
+
+// extra lines of loads in flight ahead of use in the marches (A/B r06j at 4096^2: 0 / 1 / 2 ->
+// PCG 4,684 / 4,614 / 4,523 it/s, BiCGSTAB 2,133 / 2,085 / 2,052: the one-line pipeline is enough)
+#ifndef GK_SR_PD
+#define GK_SR_PD 0
+#endif
+constexpr int PD = GK_SR_PD;
 
 template <int VEC, int K>
 __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
@@ -212,58 +242,115 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
     double acc0 = 0.0, acc1 = 0.0;
 
     auto in_ptr = [&](int v) -> const double * { return v == 0 ? a.in0 : v == 1 ? a.in1 : a.in2; };
-    // operand line jj: u (and t = u/d for the cbpr2 passes)
-    auto load_line = [&](int jj, double (&u)[VEC], double (&t)[VEC]) {
-        double v[3][VEC];
+    // Software pipeline: the raw operand inputs of line j+2 and the epilogue and
+    // edge-lane inputs of line j+1 are issued at the top of step j and consumed in
+    // step j+1.  Every load is unconditional (addresses clamped to valid memory,
+    // out-of-range values replaced by selects afterwards), so the compiler can wait
+    // for exactly the loads a step consumes instead of draining the pipeline at a
+    // branch merge.
+    const i64 il = act ? i0 : 0;  // the load column (a lane past N loads column 0, then writes nothing)
+    auto ldr = [&](const double *p, double (&v)[VEC]) {
+        if constexpr (VEC == 2) {
+            const double2 t = *reinterpret_cast<const double2 *>(p);
+            v[0] = t.x;
+            v[1] = t.y;
+        } else {
+            v[0] = p[0];
+        }
+    };
+    // line jj of input q: own line, halo line, or the zero line past a physical
+    // boundary (the operand of zero inputs is +0 in every formula: no select).
+    // The halo choice is made once, outside the march.
+    const double *lo_[3], *hi_[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        lo_[q] = a.lo[q] != nullptr ? a.lo[q] : a.zl;
+        hi_[q] = a.hi[q] != nullptr ? a.hi[q] : a.zl;
+    }
+    auto src = [&](int q, int jj) -> const double * {
+        return jj < 0 ? lo_[q] : (jj < a.nlines ? in_ptr(q) + (i64)jj * N : (jj == a.nlines ? hi_[q] : a.zl));
+    };
+    auto raw_line = [&](int jj, double (&v)[3][VEC]) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             if (q < NIN) {
-                const double *p = jj < 0 ? a.lo[q] : jj >= a.nlines ? a.hi[q] : in_ptr(q) + (i64)jj * N;
-                ld_vec<VEC>(p != nullptr ? p + i0 : nullptr, act && p != nullptr, v[q]);
+                ldr(src(q, jj) + il, v[q]);
             } else {
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) v[q][k] = 0.0;
             }
         }
-        // a missing line (physical boundary) is zero, whatever the operand formula
-        const bool here = jj < 0 ? a.lo[0] != nullptr : jj >= a.nlines ? a.hi[0] != nullptr : true;
+    };
+    auto form = [&](const double (&v)[3][VEC], double (&u)[VEC], double (&t)[VEC]) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-            u[k] = here ? sr_operand<K>(v[0][k], v[1][k], v[2][k], al, be, om) : 0.0;
+            const double x = sr_operand<K>(v[0][k], v[1][k], v[2][k], al, be, om);
+            u[k] = act ? x : 0.0;
             t[k] = CB ? u[k] / dv : u[k];
         }
     };
-    auto point_t = [&](i64 e) -> double {  // t at own-slab element e (W/E neighbour of an edge lane)
-        const double v0 = a.in0[e];
-        const double v1 = NIN > 1 ? a.in1[e] : 0.0;
-        const double v2 = NIN > 2 ? a.in2[e] : 0.0;
-        const double u = sr_operand<K>(v0, v1, v2, al, be, om);
+    auto edge_t = [&](const double (&e)[3]) -> double {  // t of an edge lane's W/E neighbour
+        const double u = sr_operand<K>(e[0], e[1], e[2], al, be, om);
         return CB ? u / dv : u;
+    };
+    // edge inputs of own line jj: lane 0 the point left of the window, lane 63 the
+    // one right of it; the other lanes reload a point of their own (same lines)
+    i64 ei = lane == 0 ? i0 - 1 : (lane == 63 ? i0 + VEC : i0);
+    ei = ei < 0 ? 0 : (ei >= N ? N - 1 : ei);
+    auto edge_ld = [&](int jj, double (&e)[3]) {
+        const i64 off = (i64)jj * N + ei;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) e[q] = q < NIN ? in_ptr(q)[off] : 0.0;
+    };
+    auto epi_ld = [&](int jj, double (&xv)[VEC], double (&rv)[VEC], double (&vd)[VEC]) {
+        const i64 off = (i64)jj * N + il;
+        if (K == SRK_CG_X) {
+            ldr(a.x + off, xv);
+            ldr(a.r + off, rv);
+        }
+        if (VD) ldr(a.vd + off, vd);
     };
 
     if (j0 < a.nlines) {
-        double um[VEC], uc[VEC], up[VEC], un[VEC], tm[VEC], tc[VEC], tp[VEC], tn[VEC];
-        load_line(j0 - 1, um, tm);
-        load_line(j0, uc, tc);
-        load_line(j0 + 1, up, tp);
+        double uc[VEC], up[VEC], tm[VEC], tc[VEC], tp[VEC], scratch[VEC];
+        {
+            double v[3][VEC];
+            raw_line(j0 - 1, v);
+            form(v, scratch, tm);
+            raw_line(j0, v);
+            form(v, uc, tc);
+            raw_line(j0 + 1, v);
+            form(v, up, tp);
+        }
+        // in flight: operand inputs of lines j+2 .. j+2+PD, epilogue operands of
+        // lines j+1 .. j+1+PD (PD = GK_SR_PD further lines ahead of use)
+        double rw[PD + 1][3][VEC];
+        double xq[PD + 1][VEC] = {}, rq[PD + 1][VEC] = {}, vq[PD + 1][VEC] = {};
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) un[k] = tn[k] = 0.0;
+        for (int d = 0; d < PD; ++d) {
+            raw_line(j0 + 2 + d, rw[d]);
+            epi_ld(j0 + 1 + d < j1 ? j0 + 1 + d : j0, xq[d], rq[d], vq[d]);
+        }
+        double xc[VEC] = {}, rc[VEC] = {}, vc[VEC] = {}, ec[3] = {};
+        epi_ld(j0, xc, rc, vc);
+        edge_ld(j0, ec);
         for (int j = j0; j < j1; ++j) {
-            if (j + 2 <= j1) load_line(j + 2, un, tn);
+            // issue: operand inputs of line j+2+PD (unused past the block's last line),
+            // epilogue inputs of line j+1+PD and edge inputs of line j+1 (line j stands in past the last)
+            const int jn = j + 1 < j1 ? j + 1 : j;
+            const int je = j + 1 + PD < j1 ? j + 1 + PD : j;
+            raw_line(j + 2 + PD, rw[PD]);
+            epi_ld(je, xq[PD], rq[PD], vq[PD]);
+            double en[3] = {};
+            edge_ld(jn, en);
             const i64 row = (i64)j * N;
             double left = __shfl_up(tc[VEC - 1], 1, 64);
             double right = __shfl_down(tc[0], 1, 64);
-            if (lane == 0 && act) left = (i0 > 0) ? point_t(row + i0 - 1) : 0.0;
-            if (lane == 63 && act) right = (i0 + VEC < N) ? point_t(row + i0 + VEC) : 0.0;
-            if (i0 == 0) left = 0.0;
-            if (i0 + VEC >= N) right = 0.0;
-            // epilogue operands, issued with the line loads
-            double xv[VEC], rv[VEC], vd[VEC];
-            if (K == SRK_CG_X) {
-                ld_vec<VEC>(a.x + row + i0, act, xv);
-                ld_vec<VEC>(a.r + row + i0, act, rv);
-            }
-            if (VD) ld_vec<VEC>(a.vd + row + i0, act, vd);
+            const double et = edge_t(ec);
+            left = lane == 0 ? et : left;
+            right = lane == 63 ? et : right;
+            left = i0 == 0 ? 0.0 : left;
+            right = i0 + VEC >= N ? 0.0 : right;
             double yv[VEC];
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
@@ -277,41 +364,59 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
                     yv[k] = ax;
                 }
                 if constexpr (K == SRK_CG_X) {
-                    xv[k] = xv[k] + al * uc[k];
-                    rv[k] = rv[k] - al * ax;
+                    xc[k] = xc[k] + al * uc[k];
+                    rc[k] = rc[k] - al * ax;
                 }
             }
             if (act) {
                 if (WU) st_vec<VEC>(a.ou + row + i0, uc);
                 if (WY) st_vec<VEC>(a.oy + row + i0, yv);
                 if (K == SRK_CG_X) {
-                    st_vec<VEC>(a.x + row + i0, xv);
-                    st_vec<VEC>(a.r + row + i0, rv);
-                }
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    if constexpr (K == SRK_CG_P) acc0 = acc0 + yv[k] * uc[k];
-                    else if constexpr (K == SRK_CG_X) acc0 = acc0 + rv[k] * rv[k];
-                    else if constexpr (K == SRK_CG_Z) acc0 = acc0 + uc[k] * yv[k];
-                    else if constexpr (K == SRK_BI_P || K == SRK_ST1) acc0 = acc0 + yv[k] * vd[k];
-                    else if constexpr (K == SRK_BI_S) {
-                        acc0 = acc0 + yv[k] * uc[k];
-                        acc1 = acc1 + yv[k] * yv[k];
-                    } else if constexpr (K == SRK_ST2) {
-                        acc0 = acc0 + yv[k] * vd[k];
-                        acc1 = acc1 + yv[k] * yv[k];
-                    }
+                    st_vec<VEC>(a.x + row + i0, xc);
+                    st_vec<VEC>(a.r + row + i0, rc);
                 }
             }
 #pragma unroll
+            for (int k = 0; k < VEC; ++k) {  // a lane past N contributes exact zeros (u = 0)
+                if constexpr (K == SRK_CG_P) acc0 = acc0 + yv[k] * uc[k];
+                else if constexpr (K == SRK_CG_X) acc0 = act ? acc0 + rc[k] * rc[k] : acc0;
+                else if constexpr (K == SRK_CG_Z) acc0 = act ? acc0 + uc[k] * yv[k] : acc0;
+                else if constexpr (K == SRK_BI_P || K == SRK_ST1) acc0 = act ? acc0 + yv[k] * vc[k] : acc0;
+                else if constexpr (K == SRK_BI_S) {
+                    acc0 = act ? acc0 + yv[k] * uc[k] : acc0;
+                    acc1 = act ? acc1 + yv[k] * yv[k] : acc1;
+                } else if constexpr (K == SRK_ST2) {
+                    acc0 = act ? acc0 + yv[k] * vc[k] : acc0;
+                    acc1 = act ? acc1 + yv[k] * yv[k] : acc1;
+                }
+            }
+            // line j+2's operand, formed now that line j is done; the rings advance
+            double un[VEC], tn[VEC];
+            form(rw[0], un, tn);
+#pragma unroll
             for (int k = 0; k < VEC; ++k) {
-                um[k] = uc[k];
                 tm[k] = tc[k];
                 uc[k] = up[k];
                 tc[k] = tp[k];
                 up[k] = un[k];
                 tp[k] = tn[k];
+                xc[k] = xq[0][k];
+                rc[k] = rq[0][k];
+                vc[k] = vq[0][k];
             }
+#pragma unroll
+            for (int d = 0; d < PD; ++d) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) rw[d][q][k] = rw[d + 1][q][k];
+                    xq[d][k] = xq[d + 1][k];
+                    rq[d][k] = rq[d + 1][k];
+                    vq[d][k] = vq[d + 1][k];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) ec[q] = en[q];
         }
     }
     if constexpr (NACC > 0)

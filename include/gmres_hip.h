@@ -451,6 +451,9 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          carries the reference's normalisation rounding (the v_err band of
  *                          DESIGN.md 4.3 becomes two-sided); the step runs unfused.  A
  *                          diagnostic mode: one sequential pass per norm (~0.1 ms per 16 K)
+ *   GK_TUNE_SR_BLOCKS      target workgroups of the short-recurrence line marches (gk_sr_*; 0 =
+ *                          auto, 512: each marches JT = lines x windows / 512 grid lines, up to
+ *                          256 -- long marches re-read fewer neighbour lines)
  *   GK_TUNE_SPIN_WAIT      1 (default): gk_mgs_step_wait / gk_hh_step_wait spin on the step's
  *                          event; 0: hipEventSynchronize (may sleep in the driver per step) */
 #define GK_TUNE_PROJ_NT 0
@@ -481,6 +484,7 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_HH_NORM_ORDER 25
 #define GK_TUNE_RES_LOOKAHEAD 26
 #define GK_TUNE_RES_PF 27
+#define GK_TUNE_SR_BLOCKS 28
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 /* Test hook: hold = 1 enqueues on the context's stream a wait for a mapped host
  * word that only hold = 0 writes (hipStreamWaitValue32) -- every later kernel of

@@ -405,6 +405,9 @@ def test_short_recurrence_solvers_vs_reference_run(solver, prec):
     assert np.max(np.abs(x - 1.0)) < 1e-6
 
 
+from tests.sr_band import BAND_F, bicgstab_band  # noqa: E402
+
+
 @pytest.mark.parametrize("N", [128, 256])
 @pytest.mark.parametrize("solver,prec", [("pcg", "identity"), ("pcg", "cbpr2"), ("pbicgstab", "identity"),
                                          ("pbicgstab", "cbpr2")])
@@ -414,11 +417,11 @@ def test_short_recurrence_history_vs_reference(solver, prec, N):
     256^2 (tests/golden/reference_runs.json "*_hist": the reference truncated
     at every iteration k, make_ref_fixtures.py; the restatement reproduces it
     bit for bit, tests/test_reference.py).  The device's dots differ from the
-    reference's running sums only in summation order.  Tolerance tiers from
-    the restatement against itself at 1 vs 8 threads: PCG 1e-8 relative while
-    the residual is above 1e-4, 5e-2 below; BiCGSTAB -- whose recurrence
-    amplifies reduction-order differences -- 1e-9 over its first decade, then
-    convergence to tol with the iteration count within 15 %."""
+    reference's running sums only in summation order.  PCG: 1e-8 relative
+    while the residual is above 1e-4, 5e-2 below (the reference against itself
+    at 1 vs 8 threads: <= 1.3e-12 until the last iterations); BiCGSTAB: every
+    iteration inside the band the reference's own 1-vs-8-thread spread sets
+    (bicgstab_band), and the iteration count within 15 %."""
     import gmres_amd as ga
 
     g = REF_RUNS[f"{solver}_omp_{prec}_{N}_hist"]
@@ -439,15 +442,10 @@ def test_short_recurrence_history_vs_reference(solver, prec, N):
         assert np.all(dev <= rt), np.nonzero(dev > rt)[0][:10]
     else:
         assert abs(it - it_ref) <= max(3, 0.15 * it_ref), (it, it_ref)
-        # the first decade: the iterations BEFORE the residual first drops below r0 / 10
-        # (BiCGSTAB's residual is not monotone: a late spike above r0 / 10 is no longer
-        # comparable between reduction orders)
-        k10 = int(np.argmax(r <= 1e-1 * r[0])) if np.any(r <= 1e-1 * r[0]) else len(r)
-        early = np.arange(len(r)) < k10
-        dev = np.abs(h[early] - r[early]) / r[early]
-        print(f"\n[{solver} {prec} {N}^2] {it} vs {it_ref} iterations; max rel dev over the first decade: "
-              f"{dev.max():.2e}")
-        assert np.all(dev <= 1e-9)
+        ok, worst = bicgstab_band(h, r, np.asarray(REF_RUNS[f"{solver}_omp_{prec}_{N}_hist_t8"]["hist_res"]))
+        print(f"\n[{solver} {prec} {N}^2] {it} vs {it_ref} iterations; whole history inside the band, worst "
+              f"|ln(h/r)| / ln(1 + {BAND_F:.0f} S) = {worst:.2f}")
+        assert ok, worst
     assert np.max(np.abs(x - 1.0)) < 1e-6
 
 

@@ -39,15 +39,21 @@ def _close_early(h, r, rtol):
     return dev.max() if k10 else 0.0
 
 
-@pytest.mark.parametrize("N", [96, 63])
+@pytest.mark.parametrize("N,blocks", [(96, 0), (63, 0), (96, 16), (63, 7), (600, 64)])
 @pytest.mark.parametrize("solver,prec", CASES)
-def test_fused_matches_operation_sequence(solver, prec, N):
+def test_fused_matches_operation_sequence(solver, prec, N, blocks):
     """Fused passes vs the reference's call sequence on the same kernels: the
     same element-wise arithmetic, different dot summation trees.  N = 63 runs
-    the one-point-per-lane march (odd N)."""
+    the one-point-per-lane march (odd N); blocks > 0 (GK_TUNE_STENCIL_BLOCKS)
+    (GK_TUNE_SR_BLOCKS) sets how many lines each workgroup marches: 0 = auto (one
+    or a few lines on these grids, many at 4096^2); 16 / 7 / 64 force long marches
+    (the software pipeline's steady state); N = 600 has two windows per line."""
     import gmres_amd as ga
+    from gmres_amd import _native as nat
 
     with ga.Context(N, 8) as ctx:
+        if blocks:
+            ctx.tune(nat.GK_TUNE_SR_BLOCKS, blocks)
         ctx.set_precond(prec, (8.2, 0.2), 4)
         ctx.set_rhs_ones()
         xf, itf, rf, hf = _solve(ctx, solver, 1e-9, 4000, fused=True)
@@ -73,10 +79,13 @@ def test_chunking_is_bit_identical(solver, prec):
     histories and x."""
     import gmres_amd as ga
 
+    from gmres_amd import _native as nat
+
     N, K = 80, 40
     outs = []
     for chunks in ([1] * K, [K], [3, K - 3]):
         with ga.Context(N, 8) as ctx:
+            ctx.tune(nat.GK_TUNE_SR_BLOCKS, 16)  # several lines per workgroup
             ctx.set_precond(prec, (8.2, 0.2), 4)
             ctx.set_rhs_ones()
             s = ga.SrSolve(ctx, solver, 0.0, K)
@@ -155,9 +164,10 @@ HIST50 = [("pcg", "identity"), ("pcg", "cbpr2"), ("pbicgstab", "identity"), ("pb
 def test_4096_history_vs_reference(solver, prec):
     """Full size: the first 50 iterations at 4096^2 (the bench legs' grid)
     against the reference's own serial run truncated at every iteration
-    (make_ref_fixtures.py KHIST_CAP).  Relative 1e-9 per iteration: the
-    reference against itself at 1 vs 8 threads differs by < 1e-12 over these
-    iterations at 256^2 (see the band test)."""
+    (make_ref_fixtures.py KHIST_CAP).  PCG: relative 1e-9 per iteration (the
+    reference against itself at 1 vs 8 threads differs by < 1.3e-12 over these
+    iterations at 256^2); BiCGSTAB: the band its own 1-vs-8-thread spread sets
+    at 4096^2 ("*_4096_hist50_t8"; cbpr2 already 27 % apart at iteration 50)."""
     import gmres_amd as ga
 
     g = REF_RUNS[f"{solver}_omp_{prec}_4096_hist50"]
@@ -172,7 +182,14 @@ def test_4096_history_vs_reference(solver, prec):
     assert ex == len(ref) and done == 0
     dev = np.abs(h - ref) / ref
     print(f"\n[{solver} {prec} 4096^2] max rel dev over {len(ref)} iterations: {dev.max():.2e}")
-    assert dev.max() <= 1e-9
+    if solver == "pcg":
+        assert dev.max() <= 1e-9
+    else:  # the reference's own 1-vs-8-thread spread, widened (test_gpu_solver.bicgstab_band)
+        from tests.sr_band import bicgstab_band
+
+        ok, worst = bicgstab_band(h, ref, np.asarray(REF_RUNS[f"{solver}_omp_{prec}_4096_hist50_t8"]["hist_res"]))
+        print(f"  band: worst |ln(h/r)| / ln(1 + F S) = {worst:.2f}")
+        assert ok, worst
 
 
 def _group(N, nranks, solver, prec, tol, max_iter):

@@ -26,11 +26,16 @@ REFX = np.load(os.path.join(HERE, "golden", "reference_x.npz"))
 KNOWN = json.load(open(os.path.join(HERE, "golden", "reference_known_answers.json")))
 
 GMRES_SERIAL = sorted(k for k, v in REF.items()
-                      if not k.startswith("_") and v["threads"] == 1 and not v["cut"]
-                      and v["solver"] not in ("pcg_omp", "pbicgstab_omp"))
+                      if not k.startswith("_") and v["solver"] not in ("pcg_omp", "pbicgstab_omp")
+                      and v["threads"] == 1 and not v.get("cut", False))
 KRYLOV = sorted(k for k, v in REF.items()
                 if not k.startswith("_") and v["solver"] in ("pcg_omp", "pbicgstab_omp") and "hist_iter" not in v)
-KHIST = sorted(k for k, v in REF.items() if not k.startswith("_") and "hist_iter" in v)
+# serial truncation histories run to convergence (round 5) ...
+KHIST = sorted(k for k, v in REF.items() if not k.startswith("_") and "hist_iter" in v and "iterations" in v)
+# ... and capped at 50 iterations at 4096^2 (round 6; the *_t8 twins are 8-thread runs, the
+# band of tests/sr_band.py, not bit-comparable with a serial restatement)
+KHIST_CAP = sorted(k for k, v in REF.items()
+                   if not k.startswith("_") and "hist_iter" in v and "iterations" not in v and v["threads"] == 1)
 
 
 def _oracle_run(oracle, case, threads=1, max_cycles=1000):
@@ -87,6 +92,20 @@ def test_short_recurrence_history_oracle_vs_reference(oracle, key):
     assert it == g["iterations"] and res == g["res"]
     assert np.array_equal(np.asarray(hist[: len(g["hist_res"])]), np.array(g["hist_res"]))
     assert [np.linalg.norm(x - 1.0), np.max(np.abs(x - 1.0))] == pytest.approx(g["x_err"], rel=1e-12)
+
+
+@pytest.mark.parametrize("key", KHIST_CAP)
+def test_short_recurrence_4096_history_oracle_vs_reference(oracle, key):
+    """The first 50 iterations at 4096^2 (round 6: the fused device passes'
+    full-size pin): the restatement's per-iteration residuals equal the
+    reference's truncated runs bit for bit."""
+    g = REF[key]
+    assert len(KHIST_CAP) == 4 and g["N"] == 4096
+    K = len(g["hist_res"])
+    prec = {"identity": oracle.PREC_IDENTITY, "cbpr2": oracle.PREC_CBPR2}[g["prec"]]
+    fn = oracle.pcg if g["solver"] == "pcg_omp" else oracle.pbicgstab
+    _, it, _, hist = fn(oracle.rhs_ones(g["N"]), g["N"], 1e-9, K, prec)
+    assert np.array_equal(np.asarray(hist[:K]), np.array(g["hist_res"]))
 
 
 def test_oracle_1024_serial_three_cycles_bit_exact(oracle):
