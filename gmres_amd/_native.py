@@ -31,7 +31,6 @@ GK_TUNE_RES, GK_TUNE_RES_R2, GK_TUNE_RES_SHARE, GK_TUNE_RES_TIMEOUT_MS = 8, 9, 1
 GK_TUNE_VERR_ORDER = 14
 GK_TUNE_HH_FUSE = 15
 GK_TUNE_CHEB_STEN = 16
-GK_TUNE_RES_STEN = 17
 GK_TUNE_SPIN_WAIT = 18
 GK_TUNE_GRAPH = 19
 GK_TUNE_RES_QDEF = 20
@@ -40,7 +39,6 @@ GK_TUNE_RES_FOLD = 22
 GK_TUNE_RES_BLOCK = 23
 GK_TUNE_WATCHDOG_MS = 24
 GK_TUNE_HH_NORM_ORDER = 25
-GK_TUNE_RES_LOOKAHEAD = 26
 GK_TUNE_RES_PF = 27
 GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 (GK_KID_PROJ, GK_KID_STENCIL, GK_KID_SCALE, GK_KID_UPDATE, GK_KID_COMM, GK_KID_OTHER, GK_KID_RES, GK_KID_PREC,

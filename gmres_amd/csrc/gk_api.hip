@@ -2653,9 +2653,6 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_PROJ_NT: c->tune_nt = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_PROJ_BLOCKS: c->tune_pj_blocks = value; break;
         case GK_TUNE_STENCIL_BLOCKS: c->tune_st_blocks = value; break;
-        case GK_TUNE_PROJ_REV:  // removed in round 5 (measured no gain)
-            if (value != 0) return set_err(GK_ERR_ARG, "GK_TUNE_PROJ_REV was removed (the reversed launch-path walk)");
-            break;
         case GK_TUNE_CHEB_FUSED: c->tune_cheb_fused = value != 0; break;
         case GK_TUNE_PROJ_BLOCKED: c->tune_blocked = value != 0; break;
         case GK_TUNE_XCHG_TIMEOUT_MS:
@@ -2676,10 +2673,6 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
         case GK_TUNE_RES_WONLY: c->tune_res_wonly = value < 0 ? -1 : (value != 0); break;
         case GK_TUNE_HH_FUSE: c->tune_hh_fuse = value != 0; break;
         case GK_TUNE_CHEB_STEN: c->tune_cheb_sten = value != 0; break;
-        case GK_TUNE_RES_STEN:  // removed in round 5: measured 4 % slower (profiles/r03/ab_res_sten_r03k.jsonl)
-            if (value != 0) return set_err(GK_ERR_ARG, "GK_TUNE_RES_STEN was removed (the stencil prologue of the "
-                                                       "w-only step measured 4 %% slower)");
-            break;
         case GK_TUNE_SPIN_WAIT: c->tune_spin_wait = value != 0; break;
         case GK_TUNE_GRAPH: c->tune_graph = value != 0; break;
         case GK_TUNE_RES_QDEF: c->tune_res_qdef = value < 0 ? -1 : (value != 0); break;
@@ -2704,11 +2697,6 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
                 c->pend_res_pf = value != 0;
             else
                 c->tune_res_pf = value != 0;
-            break;
-        case GK_TUNE_RES_LOOKAHEAD:  // (round 5: measured slower than the plain blocked step, removed)
-            if (value != 0)
-                return set_err(GK_ERR_ARG, "GK_TUNE_RES_LOOKAHEAD was removed (look-ahead blocked step measured slower: "
-                                           "profiles/r05/ab_lookahead_r05qr.txt)");
             break;
         case GK_TUNE_VERR_ORDER: c->tune_verr_order = value != 0; break;
         case GK_TUNE_RES_TIMEOUT_MS:

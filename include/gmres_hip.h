@@ -358,8 +358,9 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          non-temporal when a vector exceeds 48 MiB)
  *   GK_TUNE_PROJ_BLOCKS    workgroups of the projection kernel (0 = auto)
  *   GK_TUNE_STENCIL_BLOCKS target workgroups of the stencil sweeps (0 = auto)
- *   GK_TUNE_PROJ_REV       removed in round 5 (1 is refused): the alternating traversal of
- *                          successive projection launches
+ *   (keys 3, 17 and 26 -- the reversed projection walk, the w-only step's stencil
+ *   prologue and the look-ahead blocked step -- were measured slower and removed in
+ *   round 5; DESIGN.md 3.1 / 3.1c / 3.4 keep the numbers; they are unknown keys now)
  *   GK_TUNE_PROJ_BLOCKED   1: contiguous range per workgroup; 0: grid-stride
  *   GK_TUNE_PROJ_UNROLL    double2 loads in flight per thread and array: 2, 4, 8; 0 = auto
  *   GK_TUNE_CHEB_FUSED     1 (default): Chebyshev(k <= 8) as temporal-blocked passes of up to
@@ -394,8 +395,6 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *   GK_TUNE_CHEB_STEN      1 (default): the Arnoldi step's Chebyshev(k <= 8) pass forms z = A v
  *                          itself in a stage ahead of its levels (no stencil launch, no z vector;
  *                          N >= 128, slabs of at least k + 1 lines); 0: stencil launch + pass
- *   GK_TUNE_RES_STEN       removed in round 5 (1 is refused): the w-only step forming w = A V(:,j)
- *                          in its prologue measured 4 % slower at 4096^2
  *   GK_TUNE_GRAPH          1 (default): a launch-path MGS-R step (RCCL ranks, device-exchange ranks
  *                          with the resident step off, or one rank with it off) is captured once
  *                          per step index j as a hipGraph -- its 2j projection launches, 2j + 1
@@ -428,9 +427,6 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *                          instead of 2j.  Not bit-identical to the strict step (within the
  *                          residual-history tolerance of DESIGN.md 4.3).  MGS-R resident
  *                          steps only; Householder and the launch path stay strict.
- *   GK_TUNE_RES_LOOKAHEAD  removed in round 5 (a look-ahead build of the blocked step: parity
- *                          green, measured slower than the plain one -- DESIGN.md 3.1c); 1 is
- *                          refused
  *   GK_TUNE_RES_PF         the STRICT MGS-R step on the blocked kernel with blocks of 1
  *                          (k_mgs_blk<S = 1>: the reference's projection order, one all-gather
  *                          per projection) whose next dot column is prefetched into LDS during
@@ -459,7 +455,6 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_PROJ_NT 0
 #define GK_TUNE_PROJ_BLOCKS 1
 #define GK_TUNE_STENCIL_BLOCKS 2
-#define GK_TUNE_PROJ_REV 3
 #define GK_TUNE_PROJ_BLOCKED 4
 #define GK_TUNE_PROJ_UNROLL 5
 #define GK_TUNE_CHEB_FUSED 6
@@ -473,7 +468,6 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_VERR_ORDER 14
 #define GK_TUNE_HH_FUSE 15
 #define GK_TUNE_CHEB_STEN 16
-#define GK_TUNE_RES_STEN 17
 #define GK_TUNE_SPIN_WAIT 18
 #define GK_TUNE_GRAPH 19
 #define GK_TUNE_RES_QDEF 20
@@ -482,7 +476,6 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_RES_BLOCK 23
 #define GK_TUNE_WATCHDOG_MS 24
 #define GK_TUNE_HH_NORM_ORDER 25
-#define GK_TUNE_RES_LOOKAHEAD 26
 #define GK_TUNE_RES_PF 27
 #define GK_TUNE_SR_BLOCKS 28
 int gk_set_tuning(gk_ctx *ctx, int key, int value);

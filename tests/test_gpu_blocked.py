@@ -243,8 +243,8 @@ def test_blocked_knob_rejects_other_sizes():
         c.tune(nat.GK_TUNE_RES_BLOCK, 2)
         assert c.res_info()["blk"] == 2
         assert c.res_info(hh=True)["blk"] == 1  # the reflection chains stay strict
-        with pytest.raises(Exception, match="removed"):  # the look-ahead build (round 5, measured slower)
-            c.tune(nat.GK_TUNE_RES_LOOKAHEAD, 1)
+        with pytest.raises(Exception, match="unknown tuning key"):  # the look-ahead build (removed, round 5)
+            c.tune(26, 1)
 
 
 
