@@ -56,7 +56,7 @@ POINTS_BLOCKED = [
     ("4096^2 on 1 GPU", 1, 4096, 4096, "r05/bench_point_4096_blk4_r05l.json", 4),
     ("4096^2 on 2 GPUs", 2, 4096, 2896, "r05/bench_point_2896_blk2_r05h.json", 2),
     ("4096^2 on 4 GPUs", 4, 4096, 2048, "r05/bench_point_2048_blk2_r05h.json", 2),
-    ("4096^2 on 8 GPUs", 8, 4096, 1448, "r05/bench_point_1448_blk4_r05ae.json", 4),
+    ("4096^2 on 8 GPUs", 8, 4096, 1448, "r06/bench_point_1448_blk4_r06n.json", 4),
     ("8192^2 on 8 GPUs (config 4)", 8, 8192, 2896, "r05/bench_point_2896_blk2_r05h.json", 2),
 ]
 
@@ -135,7 +135,7 @@ def main() -> None:
     ap.add_argument("--hop-lo", type=float, default=1.0)
     ap.add_argument("--hop-hi", type=float, default=4.0)
     ap.add_argument("--coll-lo", type=float, default=5.0)
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05", "scaling_prediction_r05.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r06", "scaling_prediction_r06.json"))
     a = ap.parse_args()
     out = {"strict": predict(a.hop_lo, a.hop_hi, a.coll_lo),
            "blocked": predict(a.hop_lo, a.hop_hi, a.coll_lo, blocked=True)}
