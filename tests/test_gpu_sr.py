@@ -44,8 +44,8 @@ def _close_early(h, r, rtol):
 def test_fused_matches_operation_sequence(solver, prec, N, blocks):
     """Fused passes vs the reference's call sequence on the same kernels: the
     same element-wise arithmetic, different dot summation trees.  N = 63 runs
-    the one-point-per-lane march (odd N); blocks > 0 (GK_TUNE_STENCIL_BLOCKS)
-    (GK_TUNE_SR_BLOCKS) sets how many lines each workgroup marches: 0 = auto (one
+    the one-point-per-lane march (odd N); blocks > 0 (GK_TUNE_SR_BLOCKS) sets
+    how many lines each workgroup marches: 0 = auto (one
     or a few lines on these grids, many at 4096^2); 16 / 7 / 64 force long marches
     (the software pipeline's steady state); N = 600 has two windows per line."""
     import gmres_amd as ga
