@@ -807,11 +807,13 @@ def config_legs(ga, prof_every: int) -> list[dict]:
 # a line march read once (their neighbour lines are L1/L2 hits), outputs written once.
 SR_PASS_BYTES = {"sr_cg_p": 24, "sr_cg_x": 40, "sr_cg_z": 16, "sr_bi_p": 48, "sr_bi_pc": 40, "sr_bi_s": 32,
                  "sr_bi_sc": 32, "sr_st1": 24, "sr_st2": 24, "sr_bi_x": 64, "sr_bi_pe": 32, "sr_bi_se": 24,
-                 "sr_dot": 16}
+                 "sr_dot": 16, "sr_cg_xz": 48, "sr_bi_pz": 56, "sr_bi_sz": 40}
 # per iteration: the fused passes, and the reference's loops as written (each loop's
 # operands read once, results written once; the identity preconditioner is a copy)
-SR_ITER_BYTES = {("pcg", "identity"): (64, 152), ("pcg", "cbpr2"): (80, 200),
-                 ("pbicgstab", "identity"): (136, 240), ("pbicgstab", "cbpr2"): (184, 336)}
+SR_ITER_BYTES = {("pcg", "identity"): (64, 152), ("pcg", "cbpr2"): (72, 200),
+                 ("pbicgstab", "identity"): (136, 240), ("pbicgstab", "cbpr2"): (160, 336)}
+# (cbpr2: the two-level marches, GK_TUNE_SR_TWO_LEVEL 1 -- one-level passes 80 / 184; a leg
+# takes its fused figure from the passes that actually ran, sr_legs)
 SR_LEGS = [("pcg", "identity"), ("pcg", "cbpr2"), ("pbicgstab", "identity"), ("pbicgstab", "cbpr2")]
 
 
@@ -934,6 +936,11 @@ def sr_legs(ga, iters: int = 400, with_cpu: bool = True, tune: list[str] | None 
             dom = max(passes, key=lambda k: passes[k]["avg_launch_us"] * passes[k]["launches"])
             d = passes[dom]
             leg["passes"] = passes
+            # the fused bytes of the passes that ran (per iteration; the start's passes are < 2 %)
+            fb_run = int(round(sum(p["bytes_per_unknown"] * p["launches"] for p in passes.values()) / kp))
+            if fb_run != fb:
+                leg.update({"fused_bytes_per_unknown_iteration": fb_run,
+                            "hbm_gbps_fused": round(fb_run * n * ex / el / 1e9, 1)})
             leg["gap_us_per_iteration"] = round(el / ex * 1e6 - tot / kp, 2)
             leg["dominant"] = roof_guard({"kernel": f"gk::k_sr_march / k_sr_vec pass {dom}", "bound": "hbm",
                                           "avg_launch_us": d["avg_launch_us"], "achieved": d["GBps"],

@@ -26,6 +26,7 @@ GK_ERR_COMM = -6
 GK_TUNE_PROJ_NT = 0
 GK_TUNE_STENCIL_BLOCKS = 2
 GK_TUNE_SR_BLOCKS = 28
+GK_TUNE_SR_TWO_LEVEL = 29
 GK_TUNE_XCHG_TIMEOUT_MS = 7
 GK_TUNE_RES, GK_TUNE_RES_R2, GK_TUNE_RES_SHARE, GK_TUNE_RES_TIMEOUT_MS = 8, 9, 10, 11
 GK_TUNE_VERR_ORDER = 14
@@ -46,7 +47,7 @@ GK_PREC_IDENTITY, GK_PREC_CBPR2, GK_PREC_CHEB = 0, 1, 2
 # short-recurrence passes (GK_KID_SR + pass kind, gmres_amd/csrc/gk_sr.hpp)
 GK_KID_SR = 10
 SR_PASS_NAMES = ["sr_cg_p", "sr_cg_x", "sr_cg_z", "sr_bi_p", "sr_bi_pc", "sr_bi_s", "sr_bi_sc", "sr_st1", "sr_st2",
-                 "sr_bi_x", "sr_bi_pe", "sr_bi_se", "sr_dot"]
+                 "sr_bi_x", "sr_bi_pe", "sr_bi_se", "sr_dot", "sr_cg_xz", "sr_bi_pz", "sr_bi_sz"]
 KID_NAMES = ["proj", "stencil", "scale", "update", "comm", "other", "res", "prec", "halo", "graph"] + SR_PASS_NAMES
 GK_SR_PCG, GK_SR_BICGSTAB = 0, 1
 COMM_KINDS = {0: None, 1: "rccl", 2: "local-group", 3: "xgmi-device-exchange"}

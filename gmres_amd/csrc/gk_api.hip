@@ -164,6 +164,8 @@ struct gk_ctx {
     int vec = 2, JT = 16;
     dim3 sgrid;
     int sr_JT = 64, tune_sr_blocks = 0;  // the short-recurrence marches' geometry (gk_sr_*)
+    int tune_sr_two = 1;                 // GK_TUNE_SR_TWO_LEVEL
+    bool sr_two = false;                 // this solve runs the two-level marches (set by gk_sr_start)
     dim3 sr_sgrid;
     int np_sr = 0;
     int np_st = 0, np_pj = 0, nblk_stream = 0;
@@ -2692,6 +2694,7 @@ int gk_set_tuning(gk_ctx *c, int key, int value) {
                 c->tune_res_blk = value;
             break;
         case GK_TUNE_SR_BLOCKS: c->tune_sr_blocks = std::max(0, value); break;
+        case GK_TUNE_SR_TWO_LEVEL: c->tune_sr_two = value != 0; break;
         case GK_TUNE_RES_PF:
             if (c->cycle_mgs)
                 c->pend_res_pf = value != 0;
@@ -3186,6 +3189,7 @@ constexpr int SR_GRAPH_ITERS = 16;  // iterations per captured graph (even: the 
 
 struct SrVecs {
     double *r, *z, *r0, *p[2], *ap[2], *s, *as, *z1, *z2;
+    double *rr[2];  // two-level PCG: r by iteration parity (the pass reads r around its lines while it writes the next)
 };
 
 SrVecs sr_vecs(gk_ctx *c) {
@@ -3202,6 +3206,8 @@ SrVecs sr_vecs(gk_ctx *c) {
     v.as = col(7);
     v.z1 = c->w;
     v.z2 = c->vj;
+    v.rr[0] = col(0);
+    v.rr[1] = col(6);  // s: unused by PCG
     return v;
 }
 
@@ -3283,6 +3289,20 @@ int sr_vec(gk_ctx *c, gk::SrArgs a, int fin) {
     return GK_OK;
 }
 
+// Two-level march (single rank; same grid as the one-level marches, so the
+// partial slabs -- and every result -- are the one-level passes' bits).
+template <int K2>
+int sr_march2(gk_ctx *c, gk::SrArgs a, int fin) {
+    a.fin = fin;
+    ProfScope ps(c, GK_KID_SR + 13 + K2);
+    if (c->vec == 2)
+        gk::k_sr_march2<2, K2><<<c->sr_sgrid, gk::TPB, 0, c->st>>>(a);
+    else
+        gk::k_sr_march2<1, K2><<<c->sr_sgrid, gk::TPB, 0, c->st>>>(a);
+    LAUNCHCHK();
+    return GK_OK;
+}
+
 // out = M^-1 in by the generic preconditioner sweeps (Chebyshev(k)); with vdot
 // the last sweep's dot <out, vdot> feeds finaliser `fin`.
 int sr_prec(gk_ctx *c, const double *in, double *out, const double *vdot, int fin) {
@@ -3305,6 +3325,15 @@ int sr_pcg_iter(gk_ctx *c, int par) {
     a.in1 = v.p[par];
     a.ou = v.p[par ^ 1];
     CHK(sr_march<gk::SRK_CG_P>(c, a, gk::FIN_CG_ALPHA));
+    if (c->sr_two) {  // x += alpha p ; r -= alpha A p ; z = M^-1 r ; res, beta -- one two-level pass
+        a = sr_args(c);
+        a.in0 = v.p[par ^ 1];
+        a.x = c->x;
+        a.r = v.rr[par];
+        a.oy = v.rr[par ^ 1];
+        a.oz = v.z;
+        return sr_march2<gk::SR2_CG_XZ>(c, a, gk::FIN_CG_RES_BETA);
+    }
     // x += alpha p ; r -= alpha A p ; res = ||r|| (identity: beta = <r,r> / rz)
     a = sr_args(c);
     a.in0 = v.p[par ^ 1];
@@ -3334,7 +3363,21 @@ int sr_bicg_iter(gk_ctx *c, int par) {
     a.in1 = v.p[par];
     a.in2 = v.ap[par];
     a.ou = pn;
-    if (pk == GK_PREC_IDENTITY) {
+    if (c->sr_two) {  // z1 = M^-1 p, ap = A z1 and s, z2 = M^-1 s, as = A z2: two two-level passes
+        a.oy = v.z1;
+        a.oz = apn;
+        a.vd = v.r0;
+        CHK(sr_march2<gk::SR2_BI_P>(c, a, gk::FIN_BI_ALPHA));
+        a = sr_args(c);
+        a.in0 = v.r;
+        a.in1 = apn;
+        a.ou = v.s;
+        a.oy = v.z2;
+        a.oz = v.as;
+        CHK(sr_march2<gk::SR2_BI_S>(c, a, gk::FIN_BI_OMEGA));
+        z1 = v.z1;
+        z2 = v.z2;
+    } else if (pk == GK_PREC_IDENTITY) {
         a.oy = apn;
         a.vd = v.r0;
         CHK(sr_march<gk::SRK_BI_P>(c, a, gk::FIN_BI_ALPHA));
@@ -3359,7 +3402,9 @@ int sr_bicg_iter(gk_ctx *c, int par) {
     a.in0 = v.r;
     a.in1 = apn;
     a.ou = v.s;
-    if (pk == GK_PREC_IDENTITY) {
+    if (c->sr_two) {
+        // done above
+    } else if (pk == GK_PREC_IDENTITY) {
         a.oy = v.as;
         CHK(sr_march<gk::SRK_BI_S>(c, a, gk::FIN_BI_OMEGA));
     } else {
@@ -3480,6 +3525,14 @@ int gk_sr_start(gk_ctx *c, int solver, double tol, int max_iter) {
     if (c->sr_solver != solver && c->sr_graph != nullptr) {
         (void)hipGraphExecDestroy(c->sr_graph);
         c->sr_graph = nullptr;
+    }
+    {
+        const bool two = c->tune_sr_two != 0 && c->pkind == GK_PREC_CBPR2 && !sr_slabs(c);
+        if (two != c->sr_two && c->sr_graph != nullptr) {  // the captured graph runs the other passes
+            (void)hipGraphExecDestroy(c->sr_graph);
+            c->sr_graph = nullptr;
+        }
+        c->sr_two = two;
     }
     c->sr_solver = solver;
     c->sr_par = 0;

@@ -84,6 +84,7 @@ enum {
     FIN_BI_ALPHA = 7,  // alpha = rr0 / <ap, r0>                        (:127-129)
     FIN_BI_OMEGA = 8,  // omega = <as, s> / <as, as>                   (:145-147)
     FIN_BI_RES = 9,    // res = sqrt(<r,r>); beta = (<r,r0> / rr0) (alpha / omega); rr0 = <r,r0>  (:159-175)
+    FIN_CG_RES_BETA = 10,  // FIN_CG_RES then FIN_CG_BETA from the second slab (k_sr_march2 SR2_CG_XZ)
 };
 
 struct SrArgs {
@@ -91,7 +92,8 @@ struct SrArgs {
     const double *lo[3], *hi[3];    // halo line of each operand input (nullptr: physical boundary)
     const double *zl;               // N zeros: the line beyond a physical boundary
     double *ou;                     // the operand u itself (p, s)
-    double *oy;                     // the stencil output (ap, as, z, z1, z2)
+    double *oy;                     // the stencil output (ap, as, z, z1, z2); k_sr_march2: the level-1 output
+    double *oz;                     // k_sr_march2: the level-2 output (z, ap, as)
     double *x, *r;                  // updated in place (CG_X; BI_X)
     const double *e0;               // BI_X: as
     const double *vd;               // dot partner (r0, s)
@@ -128,7 +130,8 @@ __device__ __forceinline__ double sr_slab_sum(const double *p, int np, double *s
 __device__ __forceinline__ void sr_fin(int mode, SrDev *sd, const double *p0, const double *p1, int np,
                                        double *hist, SrMirror *mir, double *sm) {
     const double s0 = sr_slab_sum(p0, np, sm);
-    const double s1 = (mode == FIN_BI_OMEGA || mode == FIN_BI_RES) ? sr_slab_sum(p1, np, sm) : 0.0;
+    const double s1 =
+        (mode == FIN_BI_OMEGA || mode == FIN_BI_RES || mode == FIN_CG_RES_BETA) ? sr_slab_sum(p1, np, sm) : 0.0;
     if (threadIdx.x != 0) return;
     switch (mode) {
         case FIN_CG_INIT:
@@ -159,6 +162,9 @@ __device__ __forceinline__ void sr_fin(int mode, SrDev *sd, const double *p0, co
                 sd->rz = s0;
             } else if (mode == FIN_BI_RES) {
                 sd->beta = (s1 / sd->rz) * (sd->alpha / sd->omega);
+                sd->rz = s1;
+            } else if (mode == FIN_CG_RES_BETA) {
+                sd->beta = s1 / sd->rz;
                 sd->rz = s1;
             }
             mir->res = res;
@@ -464,6 +470,258 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
     }
     if constexpr (NACC > 0)
         sr_publish<NACC>(a, acc0, acc1, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, sm, &last);
+}
+
+// Two-level marches (single rank, gk_sr_* with cbpr2): the preconditioner and
+// the operator next to it in ONE pass.  Level 1 is computed one line ahead of
+// level 2 (line j+1 at step j), so level 2 finds its three lines in registers;
+// the W/E neighbours across windows come from the edge lanes, which compute the
+// level-1 value of the point beyond their window themselves (two edge columns:
+// ea next to the window, eb one further).  Every element-wise expression, the
+// stencil's association order and the per-workgroup dot order are those of the
+// one-level passes it replaces, on the same grid: the results are bit-identical
+// to SRK_CG_X + SRK_CG_Z, SRK_BI_PC + SRK_ST1, SRK_BI_SC + SRK_ST2.  Halo lines
+// of other ranks are not supported (the level-1 value of a halo line needs two
+// lines of the neighbour's inputs): N ranks keep the one-level passes.
+enum {
+    SR2_CG_XZ = 0,  // u = p; x += alpha u; v1 = r - alpha A u -> oy (next r); v2 = cbpr2(v1) -> oz (z);
+                    // dots <v1, v1>, <v1, v2>        (cg.f90:206-217; chebyshev.f90:27-37)
+    SR2_BI_P = 1,   // u = r + beta (p - omega ap) -> ou; v1 = cbpr2(u) -> oy (z1); v2 = A v1 -> oz (ap);
+                    // dot <v2, r0>                   (bicgstab.f90:121-129, 176-180)
+    SR2_BI_S = 2,   // u = r - alpha ap -> ou (s); v1 = cbpr2(u) -> oy (z2); v2 = A v1 -> oz (as);
+                    // dots <v2, u>, <v2, v2>         (bicgstab.f90:131-147)
+};
+
+template <int K2>
+constexpr int sr2_nin() {
+    return K2 == SR2_BI_P ? 3 : K2 == SR2_BI_S ? 2 : 1;
+}
+
+// A t at one point, k_stencil's order: 4 tc - (((W + E) + N) + S)   (poisson.f90:42)
+__device__ __forceinline__ double sr_ax(double tc, double W, double E, double tN, double tS) {
+    const double s = ((W + E) + tN) + tS;
+    return 4.0 * tc - 1.0 * s;
+}
+
+template <int VEC, int K2>
+__global__ __launch_bounds__(TPB) void k_sr_march2(SrArgs a) {
+    __shared__ double sm[WAVES];
+    __shared__ int last;
+    if (a.sd->done) return;
+    constexpr int NIN = sr2_nin<K2>();
+    constexpr bool CG = K2 == SR2_CG_XZ;
+    constexpr int OPK = K2 == SR2_BI_P ? SRK_BI_P : K2 == SR2_BI_S ? SRK_BI_S : SRK_CG_X;  // operand formula
+    const double al = a.sd->alpha, be = a.sd->beta, om = a.sd->omega;
+    const double dv = a.cd, ca = a.ca;
+    const int N = a.N, nl = a.nlines;
+    const int lane = threadIdx.x & 63;
+    const i64 i0 = (i64)blockIdx.x * (TPB * VEC) + (i64)VEC * threadIdx.x;
+    const bool act = i0 < N;
+    const int j0 = blockIdx.y * a.JT;
+    const int j1 = min(j0 + a.JT, nl);
+    const i64 il = act ? i0 : 0;
+    // edge columns: ea next to the window (lane 0: left, lane 63: right), eb one further
+    const bool e0l = lane == 0, e63 = lane == 63;
+    i64 ea = e0l ? i0 - 1 : (e63 ? i0 + VEC : i0);
+    i64 eb = e0l ? i0 - 2 : (e63 ? i0 + VEC + 1 : i0);
+    const bool eb_ok = e0l ? (i0 - 2 >= 0) : (e63 ? (i0 + VEC + 1 < N) : true);
+    ea = ea < 0 ? 0 : (ea >= N ? N - 1 : ea);
+    eb = eb < 0 ? 0 : (eb >= N ? N - 1 : eb);
+    const double *in[3] = {a.in0, a.in1, a.in2};
+    auto src = [&](const double *b, int jj) -> const double * {
+        return (jj >= 0 && jj < nl) ? b + (i64)jj * N : a.zl;
+    };
+    auto ld = [&](const double *p, double (&v)[VEC]) {
+        if constexpr (VEC == 2) {
+            const double2 t = sr_ld2<(GK_SR_NT & 1) != 0>(p);
+            v[0] = t.x;
+            v[1] = t.y;
+        } else {
+            v[0] = sr_ld1<(GK_SR_NT & 1) != 0>(p);
+        }
+    };
+    auto lde = [&](const double *p, double (&v)[VEC]) {
+        if constexpr (VEC == 2) {
+            const double2 t = sr_ld2<(GK_SR_NT & 8) != 0>(p);
+            v[0] = t.x;
+            v[1] = t.y;
+        } else {
+            v[0] = sr_ld1<(GK_SR_NT & 8) != 0>(p);
+        }
+    };
+    // raw operand inputs of one line: own points, ea, eb
+    struct Raw {
+        double v[3][VEC], a[3], b[3];
+    };
+    auto raw = [&](int jj, Raw &w) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if (q < NIN) {
+                const double *l = src(in[q], jj);
+                ld(l + il, w.v[q]);
+                w.a[q] = l[ea];
+                w.b[q] = l[eb];
+            } else {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) w.v[q][k] = 0.0;
+                w.a[q] = w.b[q] = 0.0;
+            }
+        }
+    };
+    // level-0 line: operand u and its stencil argument t (= u / d for cbpr2 at level 1)
+    struct Ul {
+        double u[VEC], t[VEC], ua, ta, tb;
+    };
+    auto form = [&](const Raw &w, Ul &o) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const double x = sr_operand<OPK>(w.v[0][k], w.v[1][k], w.v[2][k], al, be, om);
+            o.u[k] = act ? x : 0.0;
+            o.t[k] = CG ? o.u[k] : o.u[k] / dv;
+        }
+        o.ua = sr_operand<OPK>(w.a[0], w.a[1], w.a[2], al, be, om);
+        o.ta = CG ? o.ua : o.ua / dv;
+        const double ub = sr_operand<OPK>(w.b[0], w.b[1], w.b[2], al, be, om);
+        o.tb = eb_ok ? (CG ? ub : ub / dv) : 0.0;
+    };
+    // level-1 line: v1 and its stencil argument t2 (= v1 / d for cbpr2 at level 2)
+    struct Vl {
+        double v[VEC], t[VEC], va, ta;
+    };
+    // CG: r of one line (own points and ea) for v1 = r - alpha A p
+    struct Rl {
+        double v[VEC], a;
+    };
+    auto rld = [&](int jj, Rl &o) {
+        if constexpr (CG) {
+            const double *l = src(a.r, jj);
+            lde(l + il, o.v);
+            o.a = l[ea];
+        } else {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) o.v[k] = 0.0;
+            o.a = 0.0;
+        }
+    };
+    // level 1 at line jj (centre c, neighbours s = jj-1, n = jj+1)
+    auto lev1 = [&](int jj, const Ul &us, const Ul &uc, const Ul &un, const Rl &rr, Vl &o) {
+        double left = __shfl_up(uc.t[VEC - 1], 1, 64);
+        double right = __shfl_down(uc.t[0], 1, 64);
+        left = e0l ? uc.ta : left;
+        right = e63 ? uc.ta : right;
+        left = i0 == 0 ? 0.0 : left;
+        right = i0 + VEC >= N ? 0.0 : right;
+        const bool lv = jj >= 0 && jj < nl;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const double W = (k == 0) ? left : uc.t[k - 1];
+            const double E = (k == VEC - 1) ? right : uc.t[k + 1];
+            const double ax = sr_ax(uc.t[k], W, E, un.t[k], us.t[k]);
+            const double v = CG ? rr.v[k] - al * ax : uc.t[k] + ca * (uc.u[k] - ax);
+            o.v[k] = (lv && act) ? v : 0.0;
+            o.t[k] = CG ? o.v[k] / dv : o.v[k];
+        }
+        // the edge point ea: lane 0 -> W = eb, E = own point 0; lane 63 -> W = own point VEC-1, E = eb
+        const double Wa = e0l ? uc.tb : uc.t[VEC - 1];
+        const double Ea = e0l ? uc.t[0] : uc.tb;
+        const double axa = sr_ax(uc.ta, Wa, Ea, un.ta, us.ta);
+        const double va = CG ? rr.a - al * axa : uc.ta + ca * (uc.ua - axa);
+        o.va = lv ? va : 0.0;
+        o.ta = CG ? o.va / dv : o.va;
+    };
+    double acc0 = 0.0, acc1 = 0.0;
+    if (j0 < nl) {
+        Ul u0, u1, u2;  // lines j, j+1, j+2
+        Vl vm, vc;      // level 1 at lines j-1, j
+        Rl rc;          // CG: r of line j+1
+        {
+            Raw w0, w1, w2, w3, w4;
+            Rl ra, rb;
+            raw(j0 - 2, w0);
+            raw(j0 - 1, w1);
+            raw(j0, w2);
+            raw(j0 + 1, w3);
+            raw(j0 + 2, w4);
+            rld(j0 - 1, ra);
+            rld(j0, rb);
+            rld(j0 + 1, rc);
+            Ul um2, um1;
+            form(w0, um2);
+            form(w1, um1);
+            form(w2, u0);
+            form(w3, u1);
+            form(w4, u2);
+            lev1(j0 - 1, um2, um1, u0, ra, vm);
+            lev1(j0, um1, u0, u1, rb, vc);
+        }
+        double xc[VEC] = {}, dc[VEC] = {};
+        auto epi = [&](int jj, double (&xv)[VEC], double (&dd)[VEC]) {
+            const i64 off = (i64)jj * N + il;
+            if constexpr (CG) lde(a.x + off, xv);
+            if constexpr (K2 == SR2_BI_P) lde(a.vd + off, dd);
+        };
+        epi(j0, xc, dc);
+        for (int j = j0; j < j1; ++j) {
+            // issue: raw inputs of line j+3, r of line j+2, epilogue of line j+1 (line j stands in past the last)
+            Raw wn;
+            raw(j + 3, wn);
+            Rl rn;
+            rld(j + 2, rn);
+            double xn[VEC] = {}, dn[VEC] = {};
+            epi(j + 1 < j1 ? j + 1 : j, xn, dn);
+            Vl vp;  // level 1 at line j+1
+            lev1(j + 1, u0, u1, u2, rc, vp);
+            // level 2 at line j
+            double left = __shfl_up(vc.t[VEC - 1], 1, 64);
+            double right = __shfl_down(vc.t[0], 1, 64);
+            left = e0l ? vc.ta : left;
+            right = e63 ? vc.ta : right;
+            left = i0 == 0 ? 0.0 : left;
+            right = i0 + VEC >= N ? 0.0 : right;
+            double y[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const double W = (k == 0) ? left : vc.t[k - 1];
+                const double E = (k == VEC - 1) ? right : vc.t[k + 1];
+                const double ax = sr_ax(vc.t[k], W, E, vp.t[k], vm.t[k]);
+                y[k] = CG ? vc.t[k] + ca * (vc.v[k] - ax) : ax;
+                if constexpr (CG) xc[k] = xc[k] + al * u0.u[k];
+            }
+            const i64 row = (i64)j * N;
+            if (act) {
+                if constexpr (!CG) sr_stv<VEC>(a.ou + row + i0, u0.u);
+                sr_stv<VEC>(a.oy + row + i0, vc.v);
+                sr_stv<VEC>(a.oz + row + i0, y);
+                if constexpr (CG) sr_stv<VEC>(a.x + row + i0, xc);
+            }
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                if constexpr (CG) {  // cg_x's <r, r> then cg_z's <r, z>
+                    acc0 = act ? acc0 + vc.v[k] * vc.v[k] : acc0;
+                    acc1 = act ? acc1 + vc.v[k] * y[k] : acc1;
+                } else if constexpr (K2 == SR2_BI_P) {  // st1: <ap, r0>
+                    acc0 = act ? acc0 + y[k] * dc[k] : acc0;
+                } else {  // st2: <as, s>, <as, as>
+                    acc0 = act ? acc0 + y[k] * u0.u[k] : acc0;
+                    acc1 = act ? acc1 + y[k] * y[k] : acc1;
+                }
+            }
+            // advance: line j+3 formed now that line j is done
+            u0 = u1;
+            u1 = u2;
+            form(wn, u2);
+            vm = vc;
+            vc = vp;
+            rc = rn;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                xc[k] = xn[k];
+                dc[k] = dn[k];
+            }
+        }
+    }
+    constexpr int NACC = K2 == SR2_BI_P ? 1 : 2;
+    sr_publish<NACC>(a, acc0, acc1, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, sm, &last);
 }
 
 // Element-wise passes: grid-stride over double2 chunks, U in flight per thread.

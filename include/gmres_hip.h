@@ -58,9 +58,10 @@ extern "C" {
 #define GK_KID_GRAPH 9   /* one launch-path MGS-R step replayed as a hipGraph (its 2j projections, all-reduces, scale) */
 /* short-recurrence passes (gk_sr_*): GK_KID_SR + the pass kind of gk_sr.hpp --
  * 0 cg_p, 1 cg_x, 2 cg_z, 3 bi_p, 4 bi_pc, 5 bi_s, 6 bi_sc, 7 st1, 8 st2 (line
- * marches), 9 bi_x, 10 bi_pe, 11 bi_se, 12 dot (element-wise) */
+ * marches), 9 bi_x, 10 bi_pe, 11 bi_se, 12 dot (element-wise), 13 cg_xz, 14 bi_pz,
+ * 15 bi_sz (two-level marches: cbpr2 and the operator in one pass) */
 #define GK_KID_SR 10
-#define GK_NKID 23
+#define GK_NKID 26
 
 typedef struct gk_ctx gk_ctx;
 typedef struct gk_group gk_group;
@@ -450,6 +451,11 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
  *   GK_TUNE_SR_BLOCKS      target workgroups of the short-recurrence line marches (gk_sr_*; 0 =
  *                          auto, 512: each marches JT = lines x windows / 512 grid lines, up to
  *                          256 -- long marches re-read fewer neighbour lines)
+ *   GK_TUNE_SR_TWO_LEVEL   1 (default): with the cbpr2 preconditioner on one rank the
+ *                          short-recurrence solvers run the preconditioner and the operator
+ *                          next to it in one two-level march (PCG 2 passes per iteration,
+ *                          BiCGSTAB 3); 0: one pass each (3 / 5).  Bit-identical results;
+ *                          read by gk_sr_start
  *   GK_TUNE_SPIN_WAIT      1 (default): gk_mgs_step_wait / gk_hh_step_wait spin on the step's
  *                          event; 0: hipEventSynchronize (may sleep in the driver per step) */
 #define GK_TUNE_PROJ_NT 0
@@ -478,6 +484,7 @@ int gk_res_info(gk_ctx *ctx, int hh, long long *info);
 #define GK_TUNE_HH_NORM_ORDER 25
 #define GK_TUNE_RES_PF 27
 #define GK_TUNE_SR_BLOCKS 28
+#define GK_TUNE_SR_TWO_LEVEL 29
 int gk_set_tuning(gk_ctx *ctx, int key, int value);
 /* Test hook: hold = 1 enqueues on the context's stream a wait for a mapped host
  * word that only hold = 0 writes (hipStreamWaitValue32) -- every later kernel of

@@ -157,6 +157,47 @@ def test_sr_api_errors():
             ga.SrSolve(ctx, "pcg", 1e-9, 10)
 
 
+@pytest.mark.parametrize("N,blocks", [(96, 0), (96, 16), (63, 7), (65, 0), (129, 5), (600, 64)])
+@pytest.mark.parametrize("solver", ["pcg", "pbicgstab"])
+def test_two_level_marches_bit_identical_to_one_level(solver, N, blocks):
+    """cbpr2 on one rank: the two-level marches (k_sr_march2: preconditioner and
+    operator in one pass, level 1 one line ahead, the edge lanes computing their
+    neighbour's level-1 value) against the one-level passes they replace
+    (GK_TUNE_SR_TWO_LEVEL 0) on the same grid: the same element-wise arithmetic
+    and the same per-workgroup dot order, so every bit of the history and of x.
+    N = 65 / 129 (one point per lane) put a window edge next to the last column;
+    blocks > 0 force multi-line marches; N = 600 has two windows per line."""
+    import gmres_amd as ga
+    from gmres_amd import _native as nat
+
+    K = 60
+    outs = []
+    for two in (1, 0):
+        with ga.Context(N, 8) as ctx:
+            ctx.tune(nat.GK_TUNE_SR_TWO_LEVEL, two)
+            if blocks:
+                ctx.tune(nat.GK_TUNE_SR_BLOCKS, blocks)
+            ctx.set_precond("cbpr2", (8.2, 0.2), 1)
+            ctx.set_rhs_ones()
+            ctx.profile(1)
+            ctx.profile_reset()
+            s = ga.SrSolve(ctx, solver, 0.0, K)
+            s.iterate(K)
+            ex, done, res = s.status()
+            prof = ctx.profile_read()
+            ctx.profile(0)
+            assert (ex, done) == (K, 0)
+            outs.append((s.history(ex), ctx.get_x(), prof))
+    (h2, x2, p2), (h1, x1, p1) = outs
+    two = {"pcg": ["sr_cg_xz"], "pbicgstab": ["sr_bi_pz", "sr_bi_sz"]}[solver]
+    one = {"pcg": ["sr_cg_x", "sr_cg_z"], "pbicgstab": ["sr_bi_pc", "sr_st1", "sr_bi_sc", "sr_st2"]}[solver]
+    assert all(p2.get(k, (0, 0))[1] == K for k in two), p2  # the two-level passes ran ...
+    assert all(p2.get(k, (0, 0))[1] <= 1 for k in one), p2  # ... instead of the one-level ones (start: cg_z)
+    assert all(p1.get(k, (0, 0))[1] == 0 for k in two), p1
+    assert np.array_equal(h2, h1), np.max(np.abs(h2 - h1) / h1)
+    assert np.array_equal(x2, x1)
+
+
 HIST50 = [("pcg", "identity"), ("pcg", "cbpr2"), ("pbicgstab", "identity"), ("pbicgstab", "cbpr2")]
 
 
