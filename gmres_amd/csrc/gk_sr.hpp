@@ -4,7 +4,7 @@
 //
 // The reference runs every BLAS-1 operation as its own OpenMP loop and keeps
 // the scalars (alpha, beta, omega, the residual) in `single` blocks.  Here one
-// iteration is two (PCG, identity) to five (BiCGSTAB, cbpr2) passes over HBM:
+// iteration is two (PCG) or three (BiCGSTAB) passes over HBM:
 //
 //   * k_sr_march: a Poisson-5 line march (k_stencil's register scheme: lines
 //     j-1, j, j+1 in registers, W/E neighbours by __shfl) whose OPERAND is
@@ -12,6 +12,9 @@
 //     beta (p - omega ap), s = r - alpha ap -- so the vector update that
 //     precedes a stencil in the reference costs no pass of its own, and whose
 //     epilogue carries the element-wise updates and dots that follow it;
+//   * k_sr_march2 (cbpr2, one rank): two-level marches -- the preconditioner
+//     and the operator next to it in one pass, level 1 one line ahead of
+//     level 2 (PCG: r update + z = cbpr2(r); BiCGSTAB: z = cbpr2(p), A z);
 //   * k_sr_vec: the element-wise passes (BiCGSTAB's x / r update with its two
 //     dots), double2 streams.
 //

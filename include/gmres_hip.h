@@ -251,9 +251,10 @@ int gk_vec_lincomb(gk_ctx *ctx, int form, int out, int a, int b, int c, double s
 
 /* ------------------------------------- fused short-recurrence solvers ---- */
 /* pcg_omp (src/cg.f90:154-234) and pbicgstab_omp (src/bicgstab.f90:91-182)
- * with every scalar on the device: one iteration is 2 (PCG, identity) to 5
- * (BiCGSTAB, cbpr2) fused passes (gmres_amd/csrc/gk_sr.hpp), no host round
- * trip per dot.  They replace the call sequence the reference's solvers make
+ * with every scalar on the device: one iteration is 2 (PCG) or 3 (BiCGSTAB)
+ * fused passes (gmres_amd/csrc/gk_sr.hpp; with cbpr2 on one rank the
+ * preconditioner runs inside two-level marches; N ranks or
+ * GK_TUNE_SR_TWO_LEVEL 0: 3 / 5 passes), no host round trip per dot.  They replace the call sequence the reference's solvers make
  * through the operator / preconditioner seam (interfaces.f90:13-27): the
  * Fortran drivers pcg_drive / bicgstab_drive queue iterations in chunks and
  * read one status per chunk.  Vectors: the context's Krylov columns 0..7
