@@ -471,6 +471,82 @@ __global__ __launch_bounds__(TPBm) void k_march_st(const double *__restrict__ z,
     }
 }
 
+// cbpr2 march (the one-level cg_z pass: read r, write z = cbpr2(r), dot <r, z>), 16 B per
+// unknown; DM selects how t = r / d is formed: 0 IEEE division, 1 multiplication by 1/d
+// (timing only: not the reference's rounding), 2 one FMA correction of r * (1/d) (Markstein).
+template <int DM>
+__device__ __forceinline__ double divd(double u, double d, double dinv) {
+    if constexpr (DM == 0) return u / d;
+    else if constexpr (DM == 1) return u * dinv;
+    else {
+        const double q = u * dinv;
+        const double rr = __builtin_fma(-q, d, u);
+        return __builtin_fma(rr, dinv, q);
+    }
+}
+
+template <int DM>
+__global__ __launch_bounds__(256) void k_cbz(const double *__restrict__ r, double *__restrict__ z,
+                                             const double *__restrict__ zl, int N, int nlines, int JT, double d,
+                                             double dinv, double ca, double *part) {
+    __shared__ double sm[4];
+    const int lane = threadIdx.x & 63;
+    const i64 i0 = (i64)blockIdx.x * 512 + 2 * threadIdx.x;
+    const int j0 = blockIdx.y * JT;
+    const int j1 = min(j0 + JT, nlines);
+    auto src = [&](int jj) -> const double * { return (jj >= 0 && jj < nlines) ? r + (i64)jj * N : zl; };
+    i64 ei = lane == 0 ? i0 - 1 : (lane == 63 ? i0 + 2 : i0);
+    ei = ei < 0 ? 0 : (ei >= N ? N - 1 : ei);
+    double um[2], uc[2], up[2], tm[2], tc[2], tp[2];
+    auto ld = [&](int jj, double (&u)[2], double (&t)[2]) {
+        const double2 v = *reinterpret_cast<const double2 *>(src(jj) + i0);
+        u[0] = v.x;
+        u[1] = v.y;
+        t[0] = divd<DM>(u[0], d, dinv);
+        t[1] = divd<DM>(u[1], d, dinv);
+    };
+    ld(j0 - 1, um, tm);
+    ld(j0, uc, tc);
+    ld(j0 + 1, up, tp);
+    double ec = src(j0)[ei];
+    double acc = 0.0;
+    for (int j = j0; j < j1; ++j) {
+        const double2 rn = *reinterpret_cast<const double2 *>(src(j + 2) + i0);
+        const double en = src(j + 1)[ei];
+        double left = __shfl_up(tc[1], 1, 64);
+        double right = __shfl_down(tc[0], 1, 64);
+        const double et = divd<DM>(ec, d, dinv);
+        left = lane == 0 ? et : left;
+        right = lane == 63 ? et : right;
+        left = i0 == 0 ? 0.0 : left;
+        right = i0 + 2 >= N ? 0.0 : right;
+        double y[2];
+        for (int k = 0; k < 2; ++k) {
+            const double W = k == 0 ? left : tc[0];
+            const double E = k == 1 ? right : tc[1];
+            const double ax = 4.0 * tc[k] - 1.0 * (((W + E) + tp[k]) + tm[k]);
+            y[k] = tc[k] + ca * (uc[k] - ax);
+            acc += uc[k] * y[k];
+        }
+        *reinterpret_cast<double2 *>(z + (i64)j * N + i0) = double2{y[0], y[1]};
+        for (int k = 0; k < 2; ++k) {
+            um[k] = uc[k];
+            tm[k] = tc[k];
+            uc[k] = up[k];
+            tc[k] = tp[k];
+        }
+        up[0] = rn.x;
+        up[1] = rn.y;
+        tp[0] = divd<DM>(up[0], d, dinv);
+        tp[1] = divd<DM>(up[1], d, dinv);
+        ec = en;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) sm[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = sm[0] + sm[1] + sm[2] + sm[3];
+}
+
 // Flat stream of the same mix: out = z + beta p, dot <out, out>; grid-stride double2, U in flight.
 template <int U, int NT = 0>  // NT: 1 non-temporal stores, 2 also non-temporal loads
 __global__ __launch_bounds__(256) void k_flat(const double2 *__restrict__ z, const double2 *__restrict__ p,
@@ -615,6 +691,92 @@ static void march_st(const Bufs &b, int JT, int rot) {
     }, 24.0 * N * (double)N);
 }
 
+// The same cbpr2 march with V points per lane (V / 2 double2 loads per lane per line in flight).
+template <int V>
+__global__ __launch_bounds__(256) void k_cbzv(const double *__restrict__ r, double *__restrict__ z,
+                                              const double *__restrict__ zl, int N, int nlines, int JT, double d,
+                                              double ca, double *part) {
+    __shared__ double sm[4];
+    const int lane = threadIdx.x & 63;
+    const i64 i0 = (i64)blockIdx.x * (256 * V) + (i64)V * threadIdx.x;
+    const int j0 = blockIdx.y * JT;
+    const int j1 = min(j0 + JT, nlines);
+    auto src = [&](int jj) -> const double * { return (jj >= 0 && jj < nlines) ? r + (i64)jj * N : zl; };
+    i64 ei = lane == 0 ? i0 - 1 : (lane == 63 ? i0 + V : i0);
+    ei = ei < 0 ? 0 : (ei >= N ? N - 1 : ei);
+    double uc[V], up[V], tm[V], tc[V], tp[V];
+    auto ld = [&](int jj, double (&u)[V]) {
+#pragma unroll
+        for (int k = 0; k < V; k += 2) {
+            const double2 v = *reinterpret_cast<const double2 *>(src(jj) + i0 + k);
+            u[k] = v.x;
+            u[k + 1] = v.y;
+        }
+    };
+    {
+        double um[V];
+        ld(j0 - 1, um);
+        ld(j0, uc);
+        ld(j0 + 1, up);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            tm[k] = um[k] / d;
+            tc[k] = uc[k] / d;
+            tp[k] = up[k] / d;
+        }
+    }
+    double ec = src(j0)[ei];
+    double acc = 0.0;
+    for (int j = j0; j < j1; ++j) {
+        double rn[V];
+        ld(j + 2, rn);
+        const double en = src(j + 1)[ei];
+        double left = __shfl_up(tc[V - 1], 1, 64);
+        double right = __shfl_down(tc[0], 1, 64);
+        const double et = ec / d;
+        left = lane == 0 ? et : left;
+        right = lane == 63 ? et : right;
+        left = i0 == 0 ? 0.0 : left;
+        right = i0 + V >= N ? 0.0 : right;
+        double y[V];
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const double W = k == 0 ? left : tc[k - 1];
+            const double E = k == V - 1 ? right : tc[k + 1];
+            const double ax = 4.0 * tc[k] - 1.0 * (((W + E) + tp[k]) + tm[k]);
+            y[k] = tc[k] + ca * (uc[k] - ax);
+            acc += uc[k] * y[k];
+        }
+#pragma unroll
+        for (int k = 0; k < V; k += 2)
+            *reinterpret_cast<double2 *>(z + (i64)j * N + i0 + k) = double2{y[k], y[k + 1]};
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            tm[k] = tc[k];
+            uc[k] = up[k];
+            tc[k] = tp[k];
+            up[k] = rn[k];
+            tp[k] = rn[k] / d;
+        }
+        ec = en;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) sm[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = sm[0] + sm[1] + sm[2] + sm[3];
+}
+
+template <int V>
+static void cbzv(const Bufs &b, int JT) {
+    const int N = b.N;
+    const int gx = N / (256 * V), gy = (N + JT - 1) / JT;
+    char name[96];
+    std::snprintf(name, sizeof name, "cbz march V%d JT%d (%d wg)", V, JT, gx * gy);
+    timeit(name, b, [&] {
+        k_cbzv<V><<<dim3(gx, gy), 256>>>(b.z, b.o, b.zl, N, N, JT, 4.2, 0.2516835977628125, b.part);
+    }, 16.0 * N * (double)N);
+}
+
 int main(int argc, char **argv) {
     const int N = argc > 1 ? std::atoi(argv[1]) : 4096;
     const i64 n = (i64)N * N;
@@ -663,6 +825,29 @@ int main(int argc, char **argv) {
             std::snprintf(name, sizeof name, "k_sr_march<2,CG_P> JT%d (%d wg)", JT, gx * gy);
             timeit(name, b, [&] { gk::k_sr_march<2, gk::SRK_CG_P><<<dim3(gx, gy), gk::TPB>>>(a); }, bytes);
         }
+    }
+    if (argc > 2 && argv[2][0] == 'd') {  // the cbpr2 march: division cost
+        const int JT = 64, gx = N / 512, gy = N / JT;
+        const double d = 4.2, dinv = 1.0 / 4.2, ca = 0.2516835977628125;
+        for (int rep = 0; rep < 2; ++rep) {
+            timeit("cbz march IEEE division", b, [&] {
+                k_cbz<0><<<dim3(gx, gy), 256>>>(b.z, b.o, b.zl, N, N, JT, d, dinv, ca, b.part);
+            }, 16.0 * (double)n);
+            timeit("cbz march x (1/d) (timing only)", b, [&] {
+                k_cbz<1><<<dim3(gx, gy), 256>>>(b.z, b.o, b.zl, N, N, JT, d, dinv, ca, b.part);
+            }, 16.0 * (double)n);
+            timeit("cbz march Markstein (1 fma correction)", b, [&] {
+                k_cbz<2><<<dim3(gx, gy), 256>>>(b.z, b.o, b.zl, N, N, JT, d, dinv, ca, b.part);
+            }, 16.0 * (double)n);
+            for (int JT : {16, 32, 64, 128}) cbzv<2>(b, JT);
+            for (int JT : {16, 32, 64}) cbzv<4>(b, JT);
+            for (int JT : {8, 16, 32}) cbzv<8>(b, JT);
+            timeit("copy-like flat read1 write1 (k_flat with p = z)", b, [&] {
+                k_flat<4><<<2048, 256>>>((const double2 *)b.z, (const double2 *)b.z, (double2 *)b.o, n / 2, 0.5,
+                                         b.part);
+            }, 16.0 * (double)n);
+        }
+        return 0;
     }
     if (argc > 2 && argv[2][0] == 'x') {
         for (int rep = 0; rep < 2; ++rep)
