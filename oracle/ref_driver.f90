@@ -19,6 +19,9 @@
 !!   max_cycles = 0 / step_limit = 0: no cap.  xfile: x written as raw fp64.
 !!   env REF_TIME_CAP=<s>: also end the run at the first step of cycle 1 that
 !!   opens after <s> seconds (bounded CPU-baseline samples).
+!!   env REF_TOL=<tol>: the GMRES tol (default 1e-15).  A tol between cycle 1's
+!!   final_err(m-1) and final_err(m) ends the solve normally after exactly one
+!!   full cycle, so final_err(1:m) and x of cycle 1 are printed.
 !! Output: one "KEY values..." record per line (parsed by oracle/refrun.py).
 module ref_seam
     use interfaces, only: stencil_vector
@@ -139,6 +142,8 @@ program ref_driver
     !$omp end parallel
     write(*, '(A, A, A, A, 3I8)') 'RUN ', trim(solver), ' ', trim(prec), N, m, nthr
     tol = 1.0d-15
+    call get_environment_variable('REF_TOL', arg, status=i)
+    if (i == 0) read(arg, *) tol
     counting = .true.
     t0 = omp_get_wtime()
     select case (trim(solver))

@@ -112,6 +112,31 @@ KHIST_CAP = [
 ]
 
 
+# round 6: cycle 1 at the split grids IN FULL -- final_err(1:95) and x, which a run cut after
+# one cycle never prints.  tol between the cycle's final_err(94) and final_err(95) (both
+# ~0.00304 / ~0.00299 at these grids, tools/split_fe_dump.py) ends the solve normally at the
+# end of cycle 1 (gmres_mgsr.f90:385-389 / 409-412; gmres_hh.f90's end-of-cycle test).
+# x is kept as a sample: every X_STRIDE-th unknown.  (key, solver, N, threads, tol)
+SPLIT_FE_TOL = 0.00301
+X_STRIDE = 4099
+SPLIT_FE = [(f"{s}_identity_{N}_m95_cyc1full_t8", s, N, 8, SPLIT_FE_TOL)
+            for N in (1448, 2048, 2896) for s in ("mgsr_omp", "hh_omp")]
+
+
+def record_split_fe(key, solver, N, threads, tol):
+    t0 = time.time()
+    r = refrun.run(solver, N, 95, "identity", threads=threads, want_x=True, env={"REF_TOL": repr(tol)})
+    assert not r.cut and r.cycles_out == 1 and r.n_out == 95, (key, r.cycles_out, r.n_out)
+    idx = np.arange(0, N * N, X_STRIDE)
+    d = {"solver": solver, "N": N, "m": 95, "prec": "identity", "threads": r.threads, "tol": tol,
+         "n_out": r.n_out, "cycles": r.cycles_out, "final_err": r.final_err.tolist(), "x_err": list(r.x_err),
+         "final_res": r.final_res, "x_stride": X_STRIDE, "x_sample": r.x[idx].tolist(),
+         "note": "one full cycle (tol between final_err(94) and final_err(95)); x_sample = x[::x_stride]",
+         "wall_s": round(time.time() - t0, 2)}
+    print(f"{key}: {time.time() - t0:.1f} s", flush=True)
+    return key, d
+
+
 def record_khist_cap(key, solver, N, prec, K, threads):
     """Truncation history of iterations 1..K (K = 0: to convergence) with
     `threads` OpenMP threads per run (runs in parallel, 8 cores in all)."""
@@ -171,7 +196,7 @@ def main() -> None:
     only = None
     if "--only" in sys.argv:
         only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
-        unknown = only - {c[0] for c in SMALL + THREADED + KHIST + KHIST_CAP}
+        unknown = only - {c[0] for c in SMALL + THREADED + KHIST + KHIST_CAP + SPLIT_FE}
         if unknown:
             raise SystemExit(f"unknown cases {sorted(unknown)}")
     refrun.build()
@@ -198,6 +223,11 @@ def main() -> None:
         if (quick and c[2] > 128) or (only is not None and c[0] not in only):
             continue
         key, d = record_khist_cap(*c)
+        out[key] = d
+    for c in SPLIT_FE:
+        if quick or (only is not None and c[0] not in only):
+            continue
+        key, d = record_split_fe(*c)
         out[key] = d
     meta = {"_source": "oracle/_ref/ref_driver: the reference's own src/*.f90 (AlexanderGSC/gmres) compiled "
                        "by oracle/Makefile.ref (amdflang 22, -O3 -fopenmp -funroll-loops; interfaces.f90 "

@@ -20,8 +20,9 @@ R: 1448^2 ~ 4096^2 / 8, 2048^2 ~ 4096^2 / 4, 2896^2 ~ 4096^2 / 2 and
 
 Check: one GMRES(95) cycle (MGS-R and Householder) against a single-context
 run of the same grid AND against the reference's own cycle 1 at that grid
-(round 5 fixtures) -- cycle-1 true residual to 1e-9, final_err(1:95) to
-1e-6, x to 1e-9 (tolerances of tests/test_gpu_configs.py; the two runs differ
+(round 5 fixtures: the cycle-1 true residual to 1e-9; round 6: the reference's
+full cycle 1 -- final_err(1:95) to 1e-9 and x sampled every 4099th unknown to
+1e-9) -- against the single context: final_err(1:95) to 1e-6, x to 1e-9 (tolerances of tests/test_gpu_configs.py; the two runs differ
 only in the dot-product summation order) -- with the selected variant and
 workgroup count asserted, every Arnoldi step a resident launch, no
 launch-per-projection all-reduce, and every rank taking the same decisions.
@@ -94,6 +95,17 @@ def _ref_cycle1(N, method):
     return runs[f"{method}_omp_identity_{N}_m95_1cyc_t8"]["hist_res"][0]
 
 
+def _ref_full_cycle1(N, method):
+    """The REFERENCE's cycle 1 in full at this grid (round 6): final_err(1:95) and x
+    sampled every x_stride-th unknown, from a run whose tol ends it after exactly one
+    full cycle (tests/golden/make_ref_fixtures.py SPLIT_FE); None before those exist."""
+    import json
+    import os
+
+    runs = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_runs.json")))
+    return runs.get(f"{method}_omp_identity_{N}_m95_cyc1full_t8")
+
+
 def _compare(ref, res, xs, N=None, method=None):
     assert len({(r.n_out, r.cycles_out, r.n_cycles) for r in res}) == 1
     assert all(np.array_equal(res[0].hist_res, r.hist_res) for r in res)
@@ -101,9 +113,14 @@ def _compare(ref, res, xs, N=None, method=None):
     assert res[0].n_out == M
     assert res[0].hist_res[0] == pytest.approx(ref.hist_res[0], rel=1e-9)
     assert np.allclose(res[0].final_err[:M], ref.final_err[:M], rtol=1e-6, atol=0)
-    assert np.allclose(np.concatenate(xs), ref.x, rtol=1e-9, atol=1e-12)
-    if N is not None:  # rank 0's cycle-1 residual against the reference's own run, not only HIP's
+    x = np.concatenate(xs)
+    assert np.allclose(x, ref.x, rtol=1e-9, atol=1e-12)
+    if N is not None:  # rank 0's cycle 1 against the reference's own run, not only HIP's
         assert res[0].hist_res[0] == pytest.approx(_ref_cycle1(N, method), rel=1e-9)
+        g = _ref_full_cycle1(N, method)
+        if g is not None:  # final_err(1:95) and x (sampled) of the reference's full cycle 1
+            assert np.allclose(res[0].final_err[:M], g["final_err"], rtol=1e-9, atol=0)
+            assert np.allclose(x[:: g["x_stride"]], g["x_sample"], rtol=1e-9, atol=1e-12)
 
 
 def _check_profile(outs, method):

@@ -208,3 +208,42 @@ def test_reference_step_sample_and_cap():
     assert np.all(np.diff([r.step_t[j] for j in range(1, 9)]) > 0)
     r = refrun.run("mgsr_omp", 64, 30, "cbpr2", threads=2, max_cycles=2)
     assert r.cut and len(r.cycle_t) == 3 and len(r.hist_res) == 2 and r.hist_res[1] < r.hist_res[0]
+
+
+def test_reference_tol_ends_after_one_full_cycle(oracle):
+    """REF_TOL between cycle 1's final_err(m-1) and final_err(m) (taken from the
+    restatement's one-cycle run): the reference solve ends normally after exactly
+    one full cycle and prints final_err(1:m) -- equal to the restatement's bit for
+    bit (serial) -- and x (how the split-grid fixtures *_cyc1full_t8 are made)."""
+    from oracle import refrun
+
+    if not refrun.available():
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    N, m = 64, 30
+    for solver in ("mgsr_omp", "hh_omp"):
+        o = _oracle_run(oracle, {"N": N, "m": m, "prec": "identity", "solver": solver}, max_cycles=1)
+        fe = o.final_err[:m]
+        assert fe[m - 1] < fe[m - 2]
+        tol = float(fe[m - 2] + fe[m - 1]) / 2
+        r = refrun.run(solver, N, m, "identity", threads=1, env={"REF_TOL": repr(tol)}, want_x=True)
+        assert not r.cut and r.cycles_out == 1 and r.n_out == m
+        assert np.array_equal(r.final_err, fe)
+        assert r.x is not None and r.x.size == N * N
+
+
+@pytest.mark.parametrize("N", [1448, 2048, 2896])
+@pytest.mark.parametrize("solver", ["mgsr_omp", "hh_omp"])
+def test_split_full_cycle_fixtures_consistent(solver, N):
+    """The split grids' full cycle 1 (round 6): one cycle of 95 steps, tol
+    between final_err(94) and final_err(95), final_err(95) equal to the true
+    residual of the cycle's x, and that residual equal to the round-5 capped
+    run's cycle-1 residual (8 threads each: run-to-run reduction noise)."""
+    g = REF.get(f"{solver}_identity_{N}_m95_cyc1full_t8")
+    if g is None:
+        pytest.skip("fixture not generated")
+    fe = np.array(g["final_err"])
+    assert g["n_out"] == 95 and g["cycles"] == 1 and fe.size == 95
+    assert fe[94] < g["tol"] <= fe[93]
+    assert g["final_res"] == pytest.approx(fe[94], rel=1e-10)
+    assert g["final_res"] == pytest.approx(REF[f"{solver}_identity_{N}_m95_1cyc_t8"]["hist_res"][0], rel=1e-10)
+    assert len(g["x_sample"]) == len(range(0, N * N, g["x_stride"]))
