@@ -2133,8 +2133,16 @@ int gk_local_size(gk_ctx *c, long long *nloc) {
     return GK_OK;
 }
 
+// The short-recurrence solvers keep their vectors in the Krylov columns and their
+// state on the device: any call that changes the operator data, the right-hand
+// side or x, or that starts a GMRES cycle (which overwrites the columns), ends the
+// running gk_sr_* solve -- later gk_sr_iterate / status / history refuse until the
+// next gk_sr_start.
+static void sr_invalidate(gk_ctx *c) { c->sr_solver = -1; }
+
 int gk_set_precond(gk_ctx *c, int kind, const double *params, int nparams, int degree) {
     CHK(check_ctx(c));
+    sr_invalidate(c);
     if (kind < GK_PREC_IDENTITY || kind > GK_PREC_CHEB) return set_err(GK_ERR_ARG, "bad precond kind %d", kind);
     if (kind != GK_PREC_IDENTITY && (params == nullptr || nparams < 2))
         return set_err(GK_ERR_ARG, "precond needs params(1:2)");
@@ -2153,6 +2161,7 @@ int gk_set_precond(gk_ctx *c, int kind, const double *params, int nparams, int d
 
 int gk_set_rhs(gk_ctx *c, const double *b) {
     CHK(check_ctx(c));
+    sr_invalidate(c);
     HIPCHK(hipSetDevice(c->dev));
     HIPCHK(hipMemcpyAsync(c->b, b, sizeof(double) * c->nloc, hipMemcpyHostToDevice, c->st));
     CHK(sync_st(c));
@@ -2162,6 +2171,7 @@ int gk_set_rhs(gk_ctx *c, const double *b) {
 
 int gk_set_rhs_ones(gk_ctx *c) {
     CHK(check_ctx(c));
+    sr_invalidate(c);
     HIPCHK(hipSetDevice(c->dev));
     gk::k_fill<<<c->nblk_stream, gk::TPB, 0, c->st>>>(c->aux, 1.0, c->nloc);
     LAUNCHCHK();
@@ -2216,6 +2226,7 @@ int gk_get_basis(gk_ctx *c, int which, int col, double *out) {
 
 int gk_set_x(gk_ctx *c, const double *x) {
     CHK(check_ctx(c));
+    sr_invalidate(c);
     HIPCHK(hipSetDevice(c->dev));
     HIPCHK(hipMemcpyAsync(c->x, x, sizeof(double) * c->nloc, hipMemcpyHostToDevice, c->st));
     CHK(sync_st(c));
@@ -2246,6 +2257,7 @@ int gk_true_residual(gk_ctx *c, double *rel) {
 
 int gk_mgs_cycle_start(gk_ctx *c, double *beta) {
     CHK(check_ctx(c));
+    sr_invalidate(c);
     HIPCHK(hipSetDevice(c->dev));
     if (c->pend_res_blk != 0 || c->pend_res_pf >= 0) {  // a step change requested mid-cycle (gk_set_tuning)
         if (c->pend_res_blk != 0) c->tune_res_blk = c->pend_res_blk;
@@ -2410,6 +2422,7 @@ static int hh_pivot(gk_ctx *c, int j, double *hostout, int nout) {
 
 int gk_hh_cycle_start(gk_ctx *c, int precondition, double *g1) {
     CHK(check_ctx(c));
+    sr_invalidate(c);
     HIPCHK(hipSetDevice(c->dev));
     if (c->nranks > 1 && c->rank == 0 && c->nloc < c->m + 2)
         return set_err(GK_ERR_ARG, "Householder path needs the first slab to hold m+2 unknowns");

@@ -268,7 +268,11 @@ int gk_vec_lincomb(gk_ctx *ctx, int form, int out, int a, int b, int c, double s
  * gk_sr_status: wait = 0: for the oldest queued chunk; 1: for everything
  *   queued.  *executed = iterations run, *done = the first iteration with
  *   res < tol (0: none), *res = residual of the last executed iteration.
- * gk_sr_history: hist[0..n) = res after iterations 1..n (n <= *executed). */
+ * gk_sr_history: hist[0..n) = res after iterations 1..n (n <= *executed).
+ * gk_set_precond / gk_set_rhs(_ones) / gk_set_x / gk_mgs_cycle_start /
+ * gk_hh_cycle_start end a running solve (they change its data or reuse its
+ * vectors): gk_sr_iterate / status / history then return GK_ERR_STATE until
+ * the next gk_sr_start. */
 #define GK_SR_PCG 0
 #define GK_SR_BICGSTAB 1
 int gk_sr_start(gk_ctx *ctx, int solver, double tol, int max_iter);

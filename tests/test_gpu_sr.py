@@ -155,6 +155,22 @@ def test_sr_api_errors():
     with ga.Context(32, 6) as ctx:
         with pytest.raises(ga.GkError):
             ga.SrSolve(ctx, "pcg", 1e-9, 10)
+    # calls that change the solve's data or reuse its vectors end it
+    with ga.Context(32, 8) as ctx:
+        ctx.set_rhs_ones()
+        for end in (lambda: ctx.set_precond("cbpr2", (8.2, 0.2), 1), ctx.set_rhs_ones,
+                    lambda: ga.gmres_mgsr(ctx, 1e-15, max_cycles=1)):
+            s = ga.SrSolve(ctx, "pbicgstab", 0.0, 20)
+            s.iterate(5)
+            s.status()
+            end()
+            with pytest.raises(ga.GkError):
+                s.iterate(1)
+            with pytest.raises(ga.GkError):
+                s.status()
+        s = ga.SrSolve(ctx, "pbicgstab", 0.0, 20)  # a new start works
+        s.iterate(20)
+        assert s.status()[0] == 20
 
 
 @pytest.mark.parametrize("N,blocks", [(96, 0), (96, 16), (63, 7), (65, 0), (129, 5), (600, 64)])
