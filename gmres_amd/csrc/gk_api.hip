@@ -3293,12 +3293,12 @@ int sr_vec(gk_ctx *c, gk::SrArgs a, int fin) {
     const bool slabs = sr_slabs(c);
     a.fin = slabs ? gk::FIN_NONE : fin;
     {
-        ProfScope ps(c, GK_KID_SR + 9 + K);
+        ProfScope ps(c, GK_KID_SR + 9 + (K == gk::SRV_BI_XS ? gk::SRV_BI_X : K));
         // the grid (hence the partial count) comes from the largest slab: the same on every rank
         gk::k_sr_vec<K, 4><<<c->np_pj, gk::TPB, 0, c->st>>>(a, c->nloc);
         LAUNCHCHK();
     }
-    if (slabs) CHK(sr_fin_after(c, fin, c->np_pj, K == gk::SRV_BI_X));
+    if (slabs) CHK(sr_fin_after(c, fin, c->np_pj, K == gk::SRV_BI_X || K == gk::SRV_BI_XS));
     return GK_OK;
 }
 
@@ -3443,6 +3443,7 @@ int sr_bicg_iter(gk_ctx *c, int par) {
     a.in2 = v.s;
     a.e0 = v.as;
     a.vd = v.r0;
+    if (z2 == v.s) return sr_vec<gk::SRV_BI_XS>(c, a, gk::FIN_BI_RES);  // identity M: z2 = s
     return sr_vec<gk::SRV_BI_X>(c, a, gk::FIN_BI_RES);
 }
 

@@ -73,6 +73,7 @@ enum {
     SRV_BI_PE = 1,  // ou = r + beta (p - omega ap)          (generic preconditioner)
     SRV_BI_SE = 2,  // ou = r - alpha ap                     (generic preconditioner)
     SRV_DOT = 3,    // dot <in0, in1>                         (solve start)
+    SRV_BI_XS = 4,  // SRV_BI_X with z2 = s (identity M: in1 == in2): one load serves both operands
 };
 
 // What the last workgroup computes from the pass's partial slab(s).
@@ -733,7 +734,8 @@ __global__ __launch_bounds__(TPB) void k_sr_vec(SrArgs a, i64 n) {
     __shared__ double sm[WAVES];
     __shared__ int last;
     if (a.sd->done) return;
-    constexpr int NACC = K == SRV_BI_X ? 2 : K == SRV_DOT ? 1 : 0;
+    constexpr bool BX = K == SRV_BI_X || K == SRV_BI_XS;
+    constexpr int NACC = BX ? 2 : K == SRV_DOT ? 1 : 0;
     const double al = a.sd->alpha, be = a.sd->beta, om = a.sd->omega;
     const i64 n2 = n >> 1;
     const i64 step = (i64)gridDim.x * TPB * U;
@@ -745,11 +747,11 @@ __global__ __launch_bounds__(TPB) void k_sr_vec(SrArgs a, i64 n) {
         for (int u = 0; u < U; ++u) {
             const i64 e = b + (i64)u * TPB;
             if (e < n2) {
-                if (K == SRV_BI_X) {
+                if (BX) {
                     v0[u] = L(a.x, e);
                     v1[u] = L(a.in0, e);  // z1
-                    v2[u] = L(a.in1, e);  // z2
                     v3[u] = L(a.in2, e);  // s
+                    v2[u] = K == SRV_BI_XS ? v3[u] : L(a.in1, e);  // z2
                     v4[u] = L(a.e0, e);   // as
                     v5[u] = L(a.vd, e);   // r0
                 } else if (K == SRV_BI_PE) {
@@ -766,7 +768,7 @@ __global__ __launch_bounds__(TPB) void k_sr_vec(SrArgs a, i64 n) {
         for (int u = 0; u < U; ++u) {
             const i64 e = b + (i64)u * TPB;
             if (e >= n2) continue;
-            if constexpr (K == SRV_BI_X) {
+            if constexpr (BX) {
                 double2 xn, rn;
                 xn.x = v0[u].x + al * v1[u].x + om * v2[u].x;
                 xn.y = v0[u].y + al * v1[u].y + om * v2[u].y;
@@ -796,7 +798,7 @@ __global__ __launch_bounds__(TPB) void k_sr_vec(SrArgs a, i64 n) {
     }
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {  // odd-length tail element
         const i64 e = n - 1;
-        if constexpr (K == SRV_BI_X) {
+        if constexpr (BX) {
             a.x[e] = a.x[e] + al * a.in0[e] + om * a.in1[e];
             const double rn = a.in2[e] - om * a.e0[e];
             a.r[e] = rn;
