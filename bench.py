@@ -854,6 +854,27 @@ def sr_cpu_baseline(solver: str, N: int, prec: str, k1: int = 4, k2: int = 0, bu
                                                                                        "omp_threads")}}
 
 
+def sr_pmc_traffic(name: str, prec: str, n: int) -> dict:
+    """The committed PMC measurement of a short-recurrence pass at 4096^2
+    (profiles/r06/pmc_sr_traffic_r06al.json: FETCH_SIZE x 2 + WRITE_SIZE per
+    unknown, median over the dispatches of `bench.py --sr-only`): `traffic` in
+    bytes per launch, or null where the pass was not measured."""
+    path = os.path.join(ROOT, "profiles", "r06", "pmc_sr_traffic_r06al.json")
+    try:
+        db = json.load(open(path))
+    except (OSError, ValueError):
+        return {"traffic": None}
+    key = name[3:] if name.startswith("sr_") else name
+    if key == "bi_x":
+        key = "bi_x_identity_after_fix" if prec == "identity" else "bi_x_cbpr2_r06an"
+    e = db.get(key)
+    if not e or n != 4096 * 4096:
+        return {"traffic": None}
+    per = e["fetch_B_per_unknown_x2"] + e.get("write_B_per_unknown", db.get("bi_x", {}).get("write_B_per_unknown", 0.0))
+    return {"traffic": round(per * n), "traffic_per_unknown": round(per, 3),
+            "traffic_source": f"profiles/r06/pmc_sr_traffic_r06al.json:{key} (FETCH_SIZE x2 + WRITE_SIZE)"}
+
+
 def sr_legs(ga, iters: int = 400, with_cpu: bool = True, tune: list[str] | None = None,
             legs: list[tuple[str, str]] | None = None) -> list[dict]:
     """SURVEY 8f rank 3 at the bench's 4096^2: pcg_omp / pbicgstab_omp on the fused
@@ -942,11 +963,13 @@ def sr_legs(ga, iters: int = 400, with_cpu: bool = True, tune: list[str] | None 
                 leg.update({"fused_bytes_per_unknown_iteration": fb_run,
                             "hbm_gbps_fused": round(fb_run * n * ex / el / 1e9, 1)})
             leg["gap_us_per_iteration"] = round(el / ex * 1e6 - tot / kp, 2)
-            leg["dominant"] = roof_guard({"kernel": f"gk::k_sr_march / k_sr_vec pass {dom}", "bound": "hbm",
+            leg["dominant"] = roof_guard({"kernel": f"gk::k_sr_march / k_sr_march2 / k_sr_vec pass {dom}",
+                                          "bound": "hbm",
                                           "avg_launch_us": d["avg_launch_us"], "achieved": d["GBps"],
                                           "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": d["frac"],
                                           "bytes_per_launch": d["bytes_per_unknown"] * n,
-                                          "timing": f"HIP events around every pass of {kp} eager iterations"})
+                                          "timing": f"HIP events around every pass of {kp} eager iterations",
+                                          **sr_pmc_traffic(dom, prec, n)})
             # A/B: the reference's operation sequence on the same device
             ka = 60 if solver == "pcg" else 40
             c.sync()
