@@ -238,6 +238,9 @@ constexpr int PD = GK_SR_PD;
 #ifndef GK_SR_NT
 #define GK_SR_NT 14  // A/B r06y + r06z at 4096^2: +7-13 % it/s on every leg over 0 (bit 0 alone: -5-11 %)
 #endif
+#ifndef GK_SR_EDGE_GROUP
+#define GK_SR_EDGE_GROUP 1
+#endif
 typedef double sr_d2v __attribute__((ext_vector_type(2)));
 template <bool NT>
 __device__ __forceinline__ double2 sr_ld2(const double *p) {
@@ -347,8 +350,13 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
         return CB ? u / dv : u;
     };
     // edge inputs of own line jj: lane 0 the point left of the window, lane 63 the
-    // one right of it; the other lanes reload a point of their own (same lines)
-    i64 ei = lane == 0 ? i0 - 1 : (lane == 63 ? i0 + VEC : i0);
+    // one right of it.  GK_SR_EDGE_GROUP: the other lanes load lane 0's point
+    // (lanes 1..31) or lane 63's (32..62), so the wave's edge load touches two
+    // cache lines and does not depend on the main load's lines staying in L2
+    // (with non-temporal main loads they do not); 0: they reload a point of their own
+    const i64 wb0 = i0 - (i64)VEC * lane;  // the wave's first point
+    i64 ei = GK_SR_EDGE_GROUP ? (lane < 32 ? wb0 - 1 : wb0 + 64 * VEC)
+                              : (lane == 0 ? i0 - 1 : (lane == 63 ? i0 + VEC : i0));
     ei = ei < 0 ? 0 : (ei >= N ? N - 1 : ei);
     auto edge_ld = [&](int jj, double (&e)[3]) {
         const i64 off = (i64)jj * N + ei;
@@ -526,8 +534,10 @@ __global__ __launch_bounds__(TPB) void k_sr_march2(SrArgs a) {
     const i64 il = act ? i0 : 0;
     // edge columns: ea next to the window (lane 0: left, lane 63: right), eb one further
     const bool e0l = lane == 0, e63 = lane == 63;
-    i64 ea = e0l ? i0 - 1 : (e63 ? i0 + VEC : i0);
-    i64 eb = e0l ? i0 - 2 : (e63 ? i0 + VEC + 1 : i0);
+    const i64 wb0 = i0 - (i64)VEC * lane;  // the wave's first point (edge loads grouped as in k_sr_march)
+    i64 ea = GK_SR_EDGE_GROUP ? (lane < 32 ? wb0 - 1 : wb0 + 64 * VEC) : (e0l ? i0 - 1 : (e63 ? i0 + VEC : i0));
+    i64 eb = GK_SR_EDGE_GROUP ? (lane < 32 ? wb0 - 2 : wb0 + 64 * VEC + 1)
+                              : (e0l ? i0 - 2 : (e63 ? i0 + VEC + 1 : i0));
     const bool eb_ok = e0l ? (i0 - 2 >= 0) : (e63 ? (i0 + VEC + 1 < N) : true);
     ea = ea < 0 ? 0 : (ea >= N ? N - 1 : ea);
     eb = eb < 0 ? 0 : (eb >= N ? N - 1 : eb);
