@@ -856,23 +856,23 @@ def sr_cpu_baseline(solver: str, N: int, prec: str, k1: int = 4, k2: int = 0, bu
 
 def sr_pmc_traffic(name: str, prec: str, n: int) -> dict:
     """The committed PMC measurement of a short-recurrence pass at 4096^2
-    (profiles/r06/pmc_sr_traffic_r06al.json: FETCH_SIZE x 2 + WRITE_SIZE per
+    (profiles/r06/pmc_sr_traffic_r06as.json: FETCH_SIZE x 2 + WRITE_SIZE per
     unknown, median over the dispatches of `bench.py --sr-only`): `traffic` in
     bytes per launch, or null where the pass was not measured."""
-    path = os.path.join(ROOT, "profiles", "r06", "pmc_sr_traffic_r06al.json")
+    path = os.path.join(ROOT, "profiles", "r06", "pmc_sr_traffic_r06as.json")
     try:
         db = json.load(open(path))
     except (OSError, ValueError):
         return {"traffic": None}
     key = name[3:] if name.startswith("sr_") else name
     if key == "bi_x":
-        key = "bi_x_identity_after_fix" if prec == "identity" else "bi_x_cbpr2_r06an"
+        key = "bi_x_identity" if prec == "identity" else "bi_x_cbpr2"
     e = db.get(key)
     if not e or n != 4096 * 4096:
         return {"traffic": None}
-    per = e["fetch_B_per_unknown_x2"] + e.get("write_B_per_unknown", db.get("bi_x", {}).get("write_B_per_unknown", 0.0))
+    per = e["fetch_B_per_unknown_x2"] + e["write_B_per_unknown"]
     return {"traffic": round(per * n), "traffic_per_unknown": round(per, 3),
-            "traffic_source": f"profiles/r06/pmc_sr_traffic_r06al.json:{key} (FETCH_SIZE x2 + WRITE_SIZE)"}
+            "traffic_source": f"profiles/r06/pmc_sr_traffic_r06as.json:{key} (FETCH_SIZE x2 + WRITE_SIZE)"}
 
 
 def sr_legs(ga, iters: int = 400, with_cpu: bool = True, tune: list[str] | None = None,
