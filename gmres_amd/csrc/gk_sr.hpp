@@ -223,12 +223,9 @@ constexpr int sr_nacc() {
     return (K == SRK_BI_S || K == SRK_ST2) ? 2 : (K == SRK_BI_PC || K == SRK_BI_SC) ? 0 : 1;
 }
 
-// extra lines of loads in flight ahead of use in the marches (A/B r06j at 4096^2: 0 / 1 / 2 ->
-// PCG 4,684 / 4,614 / 4,523 it/s, BiCGSTAB 2,133 / 2,085 / 2,052: the one-line pipeline is enough)
-#ifndef GK_SR_PD
-#define GK_SR_PD 0
-#endif
-constexpr int PD = GK_SR_PD;
+// One line of loads in flight ahead of use (A/B r06j at 4096^2: 0 / 1 / 2 extra lines ->
+// PCG 4,684 / 4,614 / 4,523 it/s, BiCGSTAB 2,133 / 2,085 / 2,052; the deeper rings were
+// removed).
 
 // Cache policy of the streamed operands (each read or written once per pass):
 // bit 0 non-temporal loads of the march operands, bit 1 non-temporal stores,
@@ -237,9 +234,6 @@ constexpr int PD = GK_SR_PD;
 // (cache lines shared with the neighbouring window) keep the default policy.
 #ifndef GK_SR_NT
 #define GK_SR_NT 14  // A/B r06y + r06z at 4096^2: +7-13 % it/s on every leg over 0 (bit 0 alone: -5-11 %)
-#endif
-#ifndef GK_SR_EDGE_GROUP
-#define GK_SR_EDGE_GROUP 1
 #endif
 typedef double sr_d2v __attribute__((ext_vector_type(2)));
 template <bool NT>
@@ -350,13 +344,12 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
         return CB ? u / dv : u;
     };
     // edge inputs of own line jj: lane 0 the point left of the window, lane 63 the
-    // one right of it.  GK_SR_EDGE_GROUP: the other lanes load lane 0's point
-    // (lanes 1..31) or lane 63's (32..62), so the wave's edge load touches two
-    // cache lines and does not depend on the main load's lines staying in L2
-    // (with non-temporal main loads they do not); 0: they reload a point of their own
+    // one right of it; the other lanes load lane 0's point (lanes 1..31) or lane
+    // 63's (32..62), so the wave's edge load touches two cache lines and never
+    // re-reads the lanes' own points through L2 (A/B r06ap: +3-5 % over every lane
+    // reloading its own point)
     const i64 wb0 = i0 - (i64)VEC * lane;  // the wave's first point
-    i64 ei = GK_SR_EDGE_GROUP ? (lane < 32 ? wb0 - 1 : wb0 + 64 * VEC)
-                              : (lane == 0 ? i0 - 1 : (lane == 63 ? i0 + VEC : i0));
+    i64 ei = lane < 32 ? wb0 - 1 : wb0 + 64 * VEC;
     ei = ei < 0 ? 0 : (ei >= N ? N - 1 : ei);
     auto edge_ld = [&](int jj, double (&e)[3]) {
         const i64 off = (i64)jj * N + ei;
@@ -383,25 +376,18 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
             raw_line(j0 + 1, v);
             form(v, up, tp);
         }
-        // in flight: operand inputs of lines j+2 .. j+2+PD, epilogue operands of
-        // lines j+1 .. j+1+PD (PD = GK_SR_PD further lines ahead of use)
-        double rw[PD + 1][3][VEC];
-        double xq[PD + 1][VEC] = {}, rq[PD + 1][VEC] = {}, vq[PD + 1][VEC] = {};
-#pragma unroll
-        for (int d = 0; d < PD; ++d) {
-            raw_line(j0 + 2 + d, rw[d]);
-            epi_ld(j0 + 1 + d < j1 ? j0 + 1 + d : j0, xq[d], rq[d], vq[d]);
-        }
+        // in flight: operand inputs of line j+2, epilogue operands of line j+1
+        double rw[3][VEC];
+        double xq[VEC] = {}, rq[VEC] = {}, vq[VEC] = {};
         double xc[VEC] = {}, rc[VEC] = {}, vc[VEC] = {}, ec[3] = {};
         epi_ld(j0, xc, rc, vc);
         edge_ld(j0, ec);
         for (int j = j0; j < j1; ++j) {
-            // issue: operand inputs of line j+2+PD (unused past the block's last line),
-            // epilogue inputs of line j+1+PD and edge inputs of line j+1 (line j stands in past the last)
+            // issue: operand inputs of line j+2 (unused past the block's last line),
+            // epilogue and edge inputs of line j+1 (line j stands in past the last)
             const int jn = j + 1 < j1 ? j + 1 : j;
-            const int je = j + 1 + PD < j1 ? j + 1 + PD : j;
-            raw_line(j + 2 + PD, rw[PD]);
-            epi_ld(je, xq[PD], rq[PD], vq[PD]);
+            raw_line(j + 2, rw);
+            epi_ld(jn, xq, rq, vq);
             double en[3] = {};
             edge_ld(jn, en);
             const i64 row = (i64)j * N;
@@ -453,7 +439,7 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
             }
             // line j+2's operand, formed now that line j is done; the rings advance
             double un[VEC], tn[VEC];
-            form(rw[0], un, tn);
+            form(rw, un, tn);
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
                 tm[k] = tc[k];
@@ -461,20 +447,9 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
                 tc[k] = tp[k];
                 up[k] = un[k];
                 tp[k] = tn[k];
-                xc[k] = xq[0][k];
-                rc[k] = rq[0][k];
-                vc[k] = vq[0][k];
-            }
-#pragma unroll
-            for (int d = 0; d < PD; ++d) {
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) rw[d][q][k] = rw[d + 1][q][k];
-                    xq[d][k] = xq[d + 1][k];
-                    rq[d][k] = rq[d + 1][k];
-                    vq[d][k] = vq[d + 1][k];
-                }
+                xc[k] = xq[k];
+                rc[k] = rq[k];
+                vc[k] = vq[k];
             }
 #pragma unroll
             for (int q = 0; q < 3; ++q) ec[q] = en[q];
@@ -535,9 +510,8 @@ __global__ __launch_bounds__(TPB) void k_sr_march2(SrArgs a) {
     // edge columns: ea next to the window (lane 0: left, lane 63: right), eb one further
     const bool e0l = lane == 0, e63 = lane == 63;
     const i64 wb0 = i0 - (i64)VEC * lane;  // the wave's first point (edge loads grouped as in k_sr_march)
-    i64 ea = GK_SR_EDGE_GROUP ? (lane < 32 ? wb0 - 1 : wb0 + 64 * VEC) : (e0l ? i0 - 1 : (e63 ? i0 + VEC : i0));
-    i64 eb = GK_SR_EDGE_GROUP ? (lane < 32 ? wb0 - 2 : wb0 + 64 * VEC + 1)
-                              : (e0l ? i0 - 2 : (e63 ? i0 + VEC + 1 : i0));
+    i64 ea = lane < 32 ? wb0 - 1 : wb0 + 64 * VEC;
+    i64 eb = lane < 32 ? wb0 - 2 : wb0 + 64 * VEC + 1;
     const bool eb_ok = e0l ? (i0 - 2 >= 0) : (e63 ? (i0 + VEC + 1 < N) : true);
     ea = ea < 0 ? 0 : (ea >= N ? N - 1 : ea);
     eb = eb < 0 ? 0 : (eb >= N ? N - 1 : eb);
