@@ -230,10 +230,13 @@ constexpr int sr_nacc() {
 // Cache policy of the streamed operands (each read or written once per pass):
 // bit 0 non-temporal loads of the march operands, bit 1 non-temporal stores,
 // bit 2 non-temporal loads in the element-wise passes, bit 3 non-temporal loads
-// of the march epilogue operands (x, r, the dot partner).  The W/E edge loads
-// (cache lines shared with the neighbouring window) keep the default policy.
+// of the march epilogue operands (x, r, the dot partner), bit 4 non-temporal
+// loads of the march operands read for the last time in the iteration (the
+// previous p / ap).  The W/E edge loads keep the default policy.  Default 30
+// (A/B r06y / r06z / r06ax at 4096^2: 14 over 0 +7-13 % on every leg; 30 over 14
+// +1-5 %; bit 0 -- every operand non-temporal -- loses 2-14 %).
 #ifndef GK_SR_NT
-#define GK_SR_NT 14  // A/B r06y + r06z at 4096^2: +7-13 % it/s on every leg over 0 (bit 0 alone: -5-11 %)
+#define GK_SR_NT 30
 #endif
 typedef double sr_d2v __attribute__((ext_vector_type(2)));
 template <bool NT>
@@ -320,10 +323,23 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
     auto src = [&](int q, int jj) -> const double * {
         return jj < 0 ? lo_[q] : (jj < a.nlines ? in_ptr(q) + (i64)jj * N : (jj == a.nlines ? hi_[q] : a.zl));
     };
+    // operand inputs read here for the last time in the iteration (p, ap of the previous
+    // iteration: CG_P in1, BI_P in1 / in2) may load non-temporally (GK_SR_NT bit 4)
+    auto ldlast = [&](const double *p, double (&v)[VEC]) {
+        if constexpr (VEC == 2) {
+            const double2 t = sr_ld2<(GK_SR_NT & 16) != 0>(p);
+            v[0] = t.x;
+            v[1] = t.y;
+        } else {
+            v[0] = sr_ld1<(GK_SR_NT & 16) != 0>(p);
+        }
+    };
     auto raw_line = [&](int jj, double (&v)[3][VEC]) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            if (q < NIN) {
+            if (q < NIN && q > 0 && (K == SRK_CG_P || K == SRK_BI_P)) {
+                ldlast(src(q, jj) + il, v[q]);
+            } else if (q < NIN) {
                 ldr(src(q, jj) + il, v[q]);
             } else {
 #pragma unroll
