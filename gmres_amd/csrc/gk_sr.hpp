@@ -232,11 +232,13 @@ constexpr int sr_nacc() {
 // bit 2 non-temporal loads in the element-wise passes, bit 3 non-temporal loads
 // of the march epilogue operands (x, r, the dot partner), bit 4 non-temporal
 // loads of the march operands read for the last time in the iteration (the
-// previous p / ap).  The W/E edge loads keep the default policy.  Default 30
-// (A/B r06y / r06z / r06ax at 4096^2: 14 over 0 +7-13 % on every leg; 30 over 14
-// +1-5 %; bit 0 -- every operand non-temporal -- loses 2-14 %).
+// previous p / ap), bit 5 the same in the two-level marches and for r in
+// BiCGSTAB's s pass.  The W/E edge loads keep the default policy.  Default 62
+// (A/B r06y / r06z / r06ax / r06az at 4096^2: 14 over 0 +7-13 % on every leg; 30
+// over 14 +1-5 %; 62 over 30 +1 % on BiCGSTAB cbpr2; bit 0 -- every operand
+// non-temporal -- loses 2-14 %).
 #ifndef GK_SR_NT
-#define GK_SR_NT 30
+#define GK_SR_NT 62
 #endif
 typedef double sr_d2v __attribute__((ext_vector_type(2)));
 template <bool NT>
@@ -337,7 +339,11 @@ __global__ __launch_bounds__(TPB) void k_sr_march(SrArgs a) {
     auto raw_line = [&](int jj, double (&v)[3][VEC]) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            if (q < NIN && q > 0 && (K == SRK_CG_P || K == SRK_BI_P)) {
+            // last use in the iteration: the previous p / ap (CG_P, BI_P in1 / in2); with bit 5
+            // also r in BiCGSTAB's s pass (BI_S in0: bi_x then overwrites it)
+            const bool last = (q > 0 && (K == SRK_CG_P || K == SRK_BI_P)) ||
+                                  ((GK_SR_NT & 32) != 0 && q == 0 && K == SRK_BI_S);
+            if (q < NIN && last) {
                 ldlast(src(q, jj) + il, v[q]);
             } else if (q < NIN) {
                 ldr(src(q, jj) + il, v[q]);
@@ -557,12 +563,26 @@ __global__ __launch_bounds__(TPB) void k_sr_march2(SrArgs a) {
     struct Raw {
         double v[3][VEC], a[3], b[3];
     };
+    auto ldl = [&](const double *p, double (&v)[VEC]) {  // last-use inputs (GK_SR_NT bit 5)
+        if constexpr (VEC == 2) {
+            const double2 t = sr_ld2<(GK_SR_NT & 32) != 0>(p);
+            v[0] = t.x;
+            v[1] = t.y;
+        } else {
+            v[0] = sr_ld1<(GK_SR_NT & 32) != 0>(p);
+        }
+    };
     auto raw = [&](int jj, Raw &w) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
+            // last use in the iteration: the previous p / ap (BI_P in1 / in2), r in the s pass (BI_S in0)
+            const bool last = (K2 == SR2_BI_P && q > 0) || (K2 == SR2_BI_S && q == 0);
             if (q < NIN) {
                 const double *l = src(in[q], jj);
-                ld(l + il, w.v[q]);
+                if (last)
+                    ldl(l + il, w.v[q]);
+                else
+                    ld(l + il, w.v[q]);
                 w.a[q] = l[ea];
                 w.b[q] = l[eb];
             } else {
