@@ -16,6 +16,18 @@ namespace gk {
 #endif
 constexpr bool CF_LVBAR = GK_CF_LVBAR != 0;
 
+// 4c - s as ONE fma: 4c is exact (a power-of-two scale), so fma(4, c, -s)
+// rounds the same real number once, exactly as (4c) - s does -- bit-identical
+// to the per-sweep kernel and the oracle, one FP64 instruction per point and
+// level fewer in the issue-bound level chain.  0: the multiply + subtract.
+#ifndef GK_CF_FMA4
+#define GK_CF_FMA4 1
+#endif
+__device__ __forceinline__ double cf_4c_minus(double c, double s) {
+    if (GK_CF_FMA4) return __builtin_fma(4.0, c, -s);
+    return 4.0 * c - s;
+}
+
 
 // Lane i gets lane i-1's value (lane 0 gets 0) / lane i+1's (lane 63 gets 0).
 __device__ __forceinline__ double cf_from_left(double v) {
@@ -196,7 +208,7 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
                 const double W0 = cf_from_left(C1), E1 = cf_from_right(C0);
                 const double s0 = ((W0 + C1) + vw[SN][0]) + vw[SS][0];
                 const double s1 = ((C0 + E1) + vw[SN][1]) + vw[SS][1];
-                const double ax0 = 4.0 * C0 - 1.0 * s0, ax1 = 4.0 * C1 - 1.0 * s1;
+                const double ax0 = cf_4c_minus(C0, s0), ax1 = cf_4c_minus(C1, s1);
                 nd0 = ax0 / a.theta;
                 nd1 = ax1 / a.theta;
                 nr0 = ax0;
@@ -245,7 +257,7 @@ __global__ __launch_bounds__(CF_W) __attribute__((amdgpu_waves_per_eu(CF_OCC, CF
                 const double W0 = cf_from_left(C1), E1 = cf_from_right(C0);
                 const double s0 = ((W0 + C1) + d[l][SN][0]) + d[l][SS][0];
                 const double s1 = ((C0 + E1) + d[l][SN][1]) + d[l][SS][1];
-                const double ad0 = 4.0 * C0 - s0, ad1 = 4.0 * C1 - s1;
+                const double ad0 = cf_4c_minus(C0, s0), ad1 = cf_4c_minus(C1, s1);
                 const double res0 = r[l][QC][0] - ad0, res1 = r[l][QC][1] - ad1;
                 double dn0 = a.c1[l] * C0 + a.c2[l] * res0, dn1 = a.c1[l] * C1 + a.c2[l] * res1;
                 // z of level 0 in the first pass equals its d (z0 = d0)
