@@ -2,6 +2,7 @@
 // Reference: the Chebyshev(k) preconditioner is build-defined (SURVEY 8a row
 // a2; README.md:11, src/preconds/chebyshev.f90:8-38 is its degree-1 cbpr2);
 // each sweep is the per-sweep kernel's arithmetic, bit for bit.
+#include <iterator>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -383,8 +384,21 @@ int occupancy(K kern, int dev) {
 // minimises  rounds x (JT + 2L)  where a round is one wave of resident
 // workgroups (occupancy x CUs): at 4096^2, L = 8 (2 waves per SIMD) JT = 80
 // gives 1924 workgroups in ONE round where 64 would need two.
+// GK_CF_JTFINE (default): every even JT from 16 to 256 is a candidate, so the
+// one round fills the resident slots as tightly as the window count allows
+// (4096^2, L = 8: JT = 78, 2014 workgroups of 96 steps, where 80 gave 1976 of 98).
+#ifndef GK_CF_JTFINE
+#define GK_CF_JTFINE 1
+#endif
 int pick_jt(int gx, int lines, int L, i64 cap) {
-    static const int jts[] = {16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 256, 384, 512, 1024, 2048, 4096, 8192};
+    static const int jts_coarse[] = {16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 256, 384, 512, 1024, 2048, 4096, 8192};
+    static const std::vector<int> jts_fine = [] {
+        std::vector<int> v;
+        for (int jt = 16; jt <= 256; jt += 2) v.push_back(jt);
+        for (int jt : {384, 512, 1024, 2048, 4096, 8192}) v.push_back(jt);
+        return v;
+    }();
+    const std::vector<int> jts = GK_CF_JTFINE ? jts_fine : std::vector<int>(std::begin(jts_coarse), std::end(jts_coarse));
     i64 best = -1;
     int JT = GK_CF_JT > 0 ? GK_CF_JT : 64;
     for (int jt : jts) {
